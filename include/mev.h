@@ -1,0 +1,154 @@
+/*
+ * mev.h -- C ABI of the MI355X-native mobile-env step engine (libmev.so).
+ *
+ * The reference (yang-peilin/mobile-env-gan) is pure Python: its hot path is
+ * MComCore.step() (mobile_env/core/base.py:230-296) calling the plugin objects
+ * RandomWaypointMovement.move (core/movement.py:42-62), OkumuraHata via
+ * Channel.calculateSNR / Channel.datarate (core/channels.py:24-27,78-83,133-146),
+ * ResourceFair.share (core/schedules.py:20-22), BoundedLogUtility
+ * (core/utilities.py:44-58), NoDeparture (core/arrival.py:28-36) and the metrics
+ * (core/metrics.py:5-28). The reference has no FFI; this header is the boundary
+ * the Python host (mobile-env-gan_amd/mobile_env/core/_native.py, ctypes) binds.
+ * Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Return 0 on success, a negative MEV_E* code on error (mev_strerror()).
+ *   - All state / output buffers are DEVICE pointers owned by the caller (the
+ *     Python host allocates them as torch tensors); the context owns only the
+ *     read-only tables it builds (channel rate table, PCG64 jump table).
+ *   - Launches are asynchronous and stream-ordered on the hipStream_t passed as
+ *     `stream` (NULL = default stream). A context is not thread-safe; use one
+ *     context per (device, stream).
+ *   - Layout (SoA, row-major, E envs, U UEs, B base stations per env):
+ *       ue_xy   int32 [E][U][2]   UE position (integer grid, entities.py:52-54)
+ *       wp_xy   int32 [E][U][2]   RandomWaypoint target; x < 0 means "no waypoint"
+ *       pcg     uint64[E][6]      numpy-PCG64 stream of the movement model:
+ *                                 {state_lo, state_hi, inc_lo, inc_hi,
+ *                                  state0_lo, state0_hi}; state0 = state right after
+ *                                 seeding (movement re-seeds each episode,
+ *                                 movement.py:16-18 with reset_rng_episode=True)
+ *       t       int32 [E]         episode time (base.py:175,280)
+ *       bs_xy   int32 [B][2] (shared) or [E][B][2] (per env)
+ *       bs_count int32 [E]        per-env number of valid BSs (NULL: all B)
+ *     outputs
+ *       obs     f32  [E][U][4]    {x/W, y/H, data rate, scaled utility}
+ *       serving i32  [E][U]       serving BS index, -1 = not connected
+ *       reward  f32  [E]          mean scaled utility (metrics.py:25-28)
+ *       done    u8   [E]          episode over after this step (base.py:407-409)
+ *       rate64  f64  [E][U]       optional (NULL): data rate in float64
+ *       util64  f64  [E][U]       optional (NULL): scaled utility in float64 (NaN if inactive)
+ *       metrics f32  [E][4]       optional (NULL): number connections, number
+ *                                 connected, mean utility, mean datarate
+ */
+#ifndef MEV_H_
+#define MEV_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEV_ABI_VERSION 1
+
+#define MEV_OK 0
+#define MEV_EINVAL (-22)   /* bad parameters / shapes */
+#define MEV_ENOMEM (-12)   /* device allocation failed */
+#define MEV_EHIP (-1000)   /* HIP runtime error (see mev_last_hip_error) */
+#define MEV_ECHANNEL (-1001) /* channel connectivity is not a prefix of d2 */
+
+/* Scenario / plugin parameters. Mirrors MComCore.default_config() (base.py:103-153):
+ * "bs" -> bs_*, "ue" -> ue_*, "utility_params" -> util_*, "arrival_params" ep_time ->
+ * arrival_exit, EP_MAX_TIME -> ep_max_time, "movement_params" width/height. */
+typedef struct mev_params {
+  int32_t num_envs;       /* E */
+  int32_t num_ues;        /* U, 1..1024 */
+  int32_t num_bs;         /* B (max per env), 1..1024 */
+  int32_t width, height;  /* map size (base.py:104) */
+  int32_t ep_max_time;    /* EP_MAX_TIME (base.py:109) */
+  int32_t arrival_start;  /* NoDeparture arrival time, 0 (arrival.py:32-33) */
+  int32_t arrival_exit;   /* NoDeparture departure time = ep_time (arrival.py:35-36) */
+  int32_t bs_per_env;     /* 0: bs_xy is [B][2]; 1: bs_xy is [E][B][2] */
+  int32_t first_step_active; /* 1: activeUsers filled at reset (custom.py:53-54);
+                                0: bare MComCore quirk, first step of an episode is a no-op */
+  int32_t movement_reseed;   /* 1: movement RNG re-seeded every episode (movement_params
+                                reset_rng_episode=True, base.py:133, movement.py:16-18);
+                                0: one stream continued across episodes */
+  double velocity;        /* UE velocity (base.py:119, custom.py:16-18) */
+  double bs_bw, bs_freq, bs_tx, bs_height;        /* base.py:117 */
+  double ue_snr_tr, ue_noise, ue_height;          /* base.py:118-123 */
+  double util_lower, util_upper;                  /* base.py:136 */
+  double util_w1, util_w2, util_w3;               /* coeffs (10, 0, 10) */
+} mev_params;
+
+typedef struct mev_state {
+  int32_t* ue_xy;
+  int32_t* wp_xy;
+  uint64_t* pcg;
+  int32_t* t;
+  const int32_t* bs_xy;
+  const int32_t* bs_count; /* may be NULL */
+} mev_state;
+
+typedef struct mev_outputs {
+  float* obs;
+  int32_t* serving;
+  float* reward;
+  uint8_t* done;
+  double* rate64;   /* may be NULL */
+  double* util64;   /* may be NULL */
+  float* metrics;   /* may be NULL */
+} mev_outputs;
+
+typedef struct mev_ctx mev_ctx;
+
+/* Library ABI version (MEV_ABI_VERSION). */
+int mev_abi_version(void);
+
+/* Build a context on the current HIP device: validates params and builds, ON THE
+ * DEVICE, the channel table (Okumura-Hata -> SNR -> Shannon rate at every integer
+ * squared distance, channels.py:24-27,78-83,133-146; replaces the per-pair
+ * Channel.calculateSNR/datarate calls of base.py:212-214,427-431) and the PCG64
+ * jump-ahead table. Replaces MComCore.__init__'s plugin construction
+ * (base.py:57-61). Synchronous. */
+int mev_create(const mev_params* params, mev_ctx** out);
+void mev_destroy(mev_ctx* ctx);
+
+/* Largest connectable squared distance (snr > snr_tr <=> d2 <= d2max); -1 if none. */
+int mev_d2max(const mev_ctx* ctx);
+/* Device pointer to the channel rate table (float64 [d2max+1]) -- for tests. */
+const double* mev_rate_table(const mev_ctx* ctx);
+/* Copy the first n entries of the channel rate table to dst (host or device memory,
+ * hipMemcpyDefault). Synchronous. */
+int mev_copy_rate_table(const mev_ctx* ctx, double* dst, int64_t n);
+
+/* Host helper: numpy-compatible seeding, np.random.default_rng(seed) ->
+ * SeedSequence(seed) -> PCG64 (movement seed = config seed + 4, base.py:156-168).
+ * Writes n rows of {state_lo, state_hi, inc_lo, inc_hi, state0_lo, state0_hi}
+ * (host memory) for non-negative seeds[i] < 2^63. */
+int mev_seed_pcg64(const uint64_t* seeds, int64_t n, uint64_t* pcg_rows);
+
+/* Reset envs: MComCore.reset + MComCustom.reset bookkeeping (base.py:172-209,
+ * custom.py:53-54) -- re-seed the movement stream, draw initial positions
+ * (movement.py:64-72), clear waypoints, t = 0. env_mask: device u8 [E] (NULL = all).
+ * Writes obs (positions, rate 0, utility 0), serving = -1. */
+int mev_reset(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
+              const uint8_t* env_mask, void* stream);
+
+/* Advance every env by `nsteps` steps of MComCore.step (base.py:230-296), one
+ * fused kernel launch per step. An env whose episode is over (t >= min(EP_MAX_TIME,
+ * departure)) is reset at the start of its next step (lazy auto-reset), so a
+ * sequence of steps reproduces the reference driver loop
+ * `reset(); step() x20; reset(); ...` (collectData2.ipynb cells 3-4). Outputs hold
+ * the last step's results. */
+int mev_step(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
+             int32_t nsteps, void* stream);
+
+/* Error text for a return code; last HIP error string for MEV_EHIP. */
+const char* mev_strerror(int code);
+const char* mev_last_hip_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEV_H_ */

@@ -1,0 +1,873 @@
+// mev_step.hip -- MI355X (gfx950) kernels + C ABI of the vectorised mobile-env step engine.
+//
+// One fused kernel per env-step implements MComCore.step (reference
+// mobile_env/core/base.py:230-296) for every env of the batch:
+//   move (RandomWaypointMovement.move, movement.py:42-62)
+//   -> associate (closest connectable BS, base.py:236-241; Channel.calculateSNR
+//      channels.py:24-27 + OkumuraHata channels.py:133-146 folded into the integer
+//      test d2 <= d2max)
+//   -> per-BS connected-UE counts (ResourceFair.share, schedules.py:20-22)
+//   -> rate = round(datarate / n, 2) (base.py:421-435, channels.py:78-83)
+//   -> scaled BoundedLogUtility (utilities.py:44-58), reward = mean utility
+//      (metrics.py:25-28), the other metrics (metrics.py:5-21)
+//   -> time / done bookkeeping (base.py:280-291,407-409; arrival.py:28-36).
+//
+// Two launch shapes:
+//   * packed: U <= 64. A wavefront holds floor(64/U) envs, one lane per UE. Per-env
+//     reductions are ballot/popcount over the env's lane segment; no LDS atomics.
+//   * block:  64 < U <= 1024. One workgroup (ceil(U/64) waves) per env; per-BS counts
+//     with LDS atomics, RNG offsets by a workgroup scan.
+// Both are HBM-streaming kernels: per UE 8+8 B state read, 8+8 B state write,
+// 16 B obs + 4 B serving write; the channel table (<= 640 KB) stays in L2.
+//
+// Numerics: the reference computes in float64 with numpy; every float64 op here keeps
+// the reference's operation order, the file is compiled with -ffp-contract=off, and
+// HIP's float64 '/', sqrt and rint are IEEE correctly rounded, so positions, serving
+// indices and the rounded rates match the reference exactly (tests/ check it).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "mev.h"
+
+typedef unsigned __int128 u128;
+
+// numpy PCG64 = PCG XSL-RR 128/64 (numpy/random/src/pcg64/pcg64.h)
+#define PCG_MULT_HI 0x2360ED051FC65DA4ULL
+#define PCG_MULT_LO 0x4385DF649FCCF645ULL
+
+namespace {
+
+constexpr int kMaxU = 1024;
+constexpr int kMaxB = 1024;
+constexpr int kKeyBits = 10;  // BS index bits in the packed (d2, bs) association key
+
+struct KParams {
+  int E, U, B, W, H;
+  int t_end, arr_start, arr_exit;
+  int first_step_active;
+  int movement_reseed;
+  int d2max;
+  int envs_per_wave;  // packed shape only
+  double Wd, Hd, vel, lower, upper, w1, w2, log_w3;
+};
+
+struct KState {
+  int2* ue_xy;
+  int2* wp_xy;
+  uint64_t* pcg;
+  int* t;
+  const int2* bs_xy;
+  const int* bs_count;
+};
+
+struct KOut {
+  float4* obs;
+  int* serving;
+  float* reward;
+  uint8_t* done;
+  double* rate64;
+  double* util64;
+  float4* metrics;
+};
+
+struct KTables {
+  const double* rate_full;  // [d2max + 1]
+  const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
+};
+
+// ------------------------------------------------------------------------------------
+// PCG64 helpers (device)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ u128 mk128(uint64_t lo, uint64_t hi) {
+  return ((u128)hi << 64) | (u128)lo;
+}
+
+__device__ __forceinline__ uint64_t pcg_output(u128 s) {
+  const uint64_t hi = (uint64_t)(s >> 64);
+  const uint64_t lo = (uint64_t)s;
+  const unsigned rot = (unsigned)(hi >> 58);
+  const uint64_t x = hi ^ lo;
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+// Advance the LCG by k steps using the jump table: s' = a^k s + G(k) inc.
+__device__ __forceinline__ u128 pcg_advance(u128 s, u128 inc, int k, const u128* jump) {
+  if (k == 0) return s;
+  const u128 m = jump[2 * k];
+  const u128 g = jump[2 * k + 1];
+  return m * s + g * inc;
+}
+
+// numpy Generator.uniform(0, span): off + scale * next_double, next_double =
+// (next_uint64 >> 11) * 2^-53 (numpy/random/src/distributions/distributions.c);
+// the reference then truncates with int() (movement.py:45-46,67-68).
+__device__ __forceinline__ int pcg_draw_coord(u128& s, u128 inc, double span) {
+  const u128 mult = mk128(PCG_MULT_LO, PCG_MULT_HI);
+  s = s * mult + inc;  // PCG64 advances, then outputs
+  const double d = (double)(pcg_output(s) >> 11) * (1.0 / 9007199254740992.0);
+  return (int)(0.0 + span * d);
+}
+
+// numpy pairwise-sum order for n <= 128 (numpy/_core/src/umath/loops_utils.h.src),
+// evaluated by lane 0 of a segment over LDS values a[0..n).
+__device__ __forceinline__ double pairwise_small(const double* a, int n) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3];
+  double r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+// numpy pairwise sum for any n: recursive halving to blocks of <= 128 (PW_BLOCKSIZE).
+__device__ double pairwise_any(const double* a, int n) {
+  if (n <= 128) return pairwise_small(a, n);
+  // explicit stack; depth <= log2(1024/128) + 1
+  struct Frame { int lo, n, stage; double left; };
+  Frame st[8];
+  int sp = 0;
+  st[0] = Frame{0, n, 0, 0.0};
+  double ret = 0.0;
+  while (sp >= 0) {
+    Frame& f = st[sp];
+    if (f.n <= 128) {
+      ret = pairwise_small(a + f.lo, f.n);
+      --sp;
+      continue;
+    }
+    int n2 = f.n / 2;
+    n2 -= n2 % 8;
+    if (f.stage == 0) {
+      f.stage = 1;
+      st[sp + 1] = Frame{f.lo, n2, 0, 0.0};
+      ++sp;
+    } else if (f.stage == 1) {
+      f.left = ret;
+      f.stage = 2;
+      st[sp + 1] = Frame{f.lo + n2, f.n - n2, 0, 0.0};
+      ++sp;
+    } else {
+      ret = f.left + ret;
+      --sp;
+    }
+  }
+  return ret;
+}
+
+// Per-UE movement (movement.py:42-62). Waypoint already drawn if needed.
+__device__ __forceinline__ void move_ue(int2& pos, int2& wp, double vel) {
+  const int dx = wp.x - pos.x;
+  const int dy = wp.y - pos.y;
+  const double nrm = sqrt((double)(dx * dx + dy * dy));  // np.linalg.norm of int vector
+  if (nrm <= vel) {  // arrived: snap to waypoint and pop it
+    pos = wp;
+    wp = make_int2(-1, -1);
+  } else {  // position + velocity * v / |v|, np.round (half-to-even), astype(int)
+    pos.x = (int)rint((double)pos.x + (vel * (double)dx) / nrm);
+    pos.y = (int)rint((double)pos.y + (vel * (double)dy) / nrm);
+  }
+}
+
+// BoundedLogUtility.calculateUtility + scaleUtility (utilities.py:44-55).
+__device__ __forceinline__ double scaled_utility(double rate, const KParams& kp) {
+  double ur;
+  if (rate <= 0.0) {
+    ur = kp.lower;
+  } else {
+    ur = kp.w1 * log(kp.w2 + rate) / kp.log_w3;
+    ur = fmin(fmax(ur, kp.lower), kp.upper);  // np.clip
+  }
+  return 2.0 * (ur - kp.lower) / (kp.upper - kp.lower) - 1.0;
+}
+
+// ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435).
+__device__ __forceinline__ double shared_rate(double full, int n) {
+  const double share = full / (double)n;
+  return rint(share * 100.0) / 100.0;
+}
+
+// ------------------------------------------------------------------------------------
+// Packed kernel: U <= 64, floor(64/U) envs per wavefront, one lane per UE.
+// RESET=true: only re-initialise envs (optionally masked), write reset obs.
+// ------------------------------------------------------------------------------------
+constexpr int kPackedBlock = 256;
+constexpr int kWavesPerBlock = kPackedBlock / 64;
+
+template <bool PER_ENV_BS, bool RESET>
+__global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
+                                                             KTables tb,
+                                                             const uint8_t* __restrict__ mask) {
+  __shared__ double lds_util[kWavesPerBlock][64];
+  __shared__ double lds_rate[kWavesPerBlock][64];
+
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const int wave = blockIdx.x * kWavesPerBlock + wib;
+  const int U = kp.U;
+  const int G = kp.envs_per_wave;
+  const int seg = lane / U;
+  const int u = lane - seg * U;
+  const int base = seg * U;
+  const int e = wave * G + seg;
+  const bool valid = (seg < G) && (e < kp.E);
+  const uint64_t segmask = (U >= 64) ? ~0ull : (((1ull << U) - 1ull) << base);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const size_t idx = (size_t)e * U + u;
+
+  int t = 0;
+  int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
+  u128 s = 0, inc = 0;
+  bool do_reset = false;
+  if (valid) {
+    const uint64_t* pr = st.pcg + (size_t)6 * e;
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(pr);
+    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(pr + 2);
+    inc = mk128(b.x, b.y);
+    if (RESET) {
+      do_reset = (mask == nullptr) || mask[e];
+    } else {
+      t = st.t[e];
+      do_reset = t >= kp.t_end;  // lazy auto-reset at the start of the next step
+    }
+    if (do_reset) {
+      // MComCore.reset (base.py:172-209): movement RNG re-seeded (movement.py:16-18),
+      // initial positions in ue_id order, 2 draws per UE (movement.py:64-72).
+      const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
+      const u128 s0 = kp.movement_reseed ? mk128(c.x, c.y) : mk128(a.x, a.y);
+      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
+      pos.x = pcg_draw_coord(su, inc, kp.Wd);
+      pos.y = pcg_draw_coord(su, inc, kp.Hd);
+      s = pcg_advance(s0, inc, 2 * U, tb.jump);
+      wp = make_int2(-1, -1);
+      t = 0;
+    } else {
+      s = mk128(a.x, a.y);
+      if (!RESET) {
+        pos = st.ue_xy[idx];
+        wp = st.wp_xy[idx];
+      }
+    }
+  }
+
+  if (RESET) {
+    if (valid && do_reset) {
+      st.ue_xy[idx] = pos;
+      st.wp_xy[idx] = wp;
+      out.serving[idx] = -1;
+      out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
+                                 0.f, 0.f);
+      if (out.rate64) out.rate64[idx] = 0.0;
+      if (out.util64) out.util64[idx] = 0.0;
+      if (u == 0) {
+        uint64_t* pw = st.pcg + (size_t)6 * e;
+        *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+        st.t[e] = 0;
+        out.reward[e] = 0.f;
+        out.done[e] = 0;
+        if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    return;
+  }
+
+  // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
+  const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
+                      (kp.first_step_active || t != 0);
+
+  // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ----------
+  const bool need = active && wp.x < 0;
+  const uint64_t mneed = __ballot(need) & segmask;
+  if (need) {
+    u128 su = pcg_advance(s, inc, 2 * __popcll(mneed & lt), tb.jump);
+    wp.x = pcg_draw_coord(su, inc, kp.Wd);
+    wp.y = pcg_draw_coord(su, inc, kp.Hd);
+  }
+  if (active) move_ue(pos, wp, kp.vel);
+
+  // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
+  unsigned best = UINT_MAX;
+  if (active) {
+    const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
+    const int2* bs = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+    for (int b = 0; b < nb; ++b) {
+      const int2 p = bs[b];
+      const int ddx = pos.x - p.x;
+      const int ddy = pos.y - p.y;
+      const unsigned key = ((unsigned)(ddx * ddx + ddy * ddy) << kKeyBits) | (unsigned)b;
+      best = min(best, key);  // ties -> lowest bs index, like python min() over stations
+    }
+  }
+  const int d2s = (int)(best >> kKeyBits);
+  const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+
+  // ---- 3. per-BS connected counts n_b within the env segment (one ballot per BS in use)
+  int n = 0;
+  {
+    uint64_t pending = __ballot(srv >= 0);
+    while (pending) {
+      const int leader = __ffsll((unsigned long long)pending) - 1;
+      const int b = __shfl(srv, leader);
+      const uint64_t mb = __ballot(srv == b);
+      if (srv == b) n = __popcll(mb & segmask);
+      pending &= ~mb;
+    }
+  }
+
+  // ---- 4. rate + utility -------------------------------------------------------------
+  double rate = 0.0;
+  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], n);
+  const double util = active ? scaled_utility(rate, kp) : 0.0;
+
+  // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) -----
+  const uint64_t mact = __ballot(active) & segmask;
+  const int nact = __popcll(mact);
+  if (active) lds_util[wib][base + __popcll(mact & lt)] = util;
+  const uint64_t mcon = __ballot(srv >= 0) & segmask;
+  const int ncon = __popcll(mcon);
+  const bool want_metrics = out.metrics != nullptr;
+  if (want_metrics && srv >= 0) lds_rate[wib][base + __popcll(mcon & lt)] = rate;
+  __syncthreads();
+
+  // ---- 6. stores ---------------------------------------------------------------------
+  if (valid) {
+    st.ue_xy[idx] = pos;
+    st.wp_xy[idx] = wp;
+    out.serving[idx] = srv;
+    out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
+                               (float)rate, (float)util);
+    if (out.rate64) out.rate64[idx] = rate;
+    if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
+    if (u == 0) {
+      const double mean_u =
+          nact > 0 ? pairwise_small(&lds_util[wib][base], nact) / (double)nact : kp.lower;
+      const u128 s_next = pcg_advance(s, inc, 2 * __popcll(mneed), tb.jump);
+      uint64_t* pw = st.pcg + (size_t)6 * e;
+      *reinterpret_cast<ulonglong2*>(pw) =
+          make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
+      st.t[e] = t + 1;
+      out.reward[e] = (float)mean_u;
+      out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
+      if (want_metrics) {
+        const double mean_r =
+            ncon > 0 ? pairwise_small(&lds_rate[wib][base], ncon) / (double)ncon : 0.0;
+        out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Block kernel: 64 < U <= 1024, one workgroup per env, lane u = threadIdx.x.
+// ------------------------------------------------------------------------------------
+template <bool PER_ENV_BS, bool RESET>
+__global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut out, KTables tb,
+                                                    const uint8_t* __restrict__ mask) {
+  __shared__ int lds_cnt[kMaxB];
+  __shared__ int lds_wtot[3][16];
+  __shared__ double lds_util[kMaxU];
+  __shared__ double lds_rate[kMaxU];
+
+  const int e = blockIdx.x;
+  const int u = threadIdx.x;
+  const int U = kp.U;
+  const int lane = u & 63;
+  const int w = u >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  const bool valid = u < U;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const size_t idx = (size_t)e * U + u;
+
+  const uint64_t* pr = st.pcg + (size_t)6 * e;
+  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(pr);
+  const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(pr + 2);
+  const u128 inc = mk128(b2.x, b2.y);
+  int t = RESET ? 0 : st.t[e];
+  const bool do_reset = RESET ? (mask == nullptr || mask[e]) : (t >= kp.t_end);
+  if (RESET && !do_reset) return;  // uniform over the workgroup
+
+  u128 s;
+  int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
+  if (do_reset) {
+    const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
+    const u128 s0 = kp.movement_reseed ? mk128(c.x, c.y) : mk128(a.x, a.y);
+    if (valid) {
+      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
+      pos.x = pcg_draw_coord(su, inc, kp.Wd);
+      pos.y = pcg_draw_coord(su, inc, kp.Hd);
+    }
+    s = pcg_advance(s0, inc, 2 * U, tb.jump);
+    t = 0;
+  } else {
+    s = mk128(a.x, a.y);
+    if (valid) {
+      pos = st.ue_xy[idx];
+      wp = st.wp_xy[idx];
+    }
+  }
+
+  if (RESET) {
+    if (valid) {
+      st.ue_xy[idx] = pos;
+      st.wp_xy[idx] = wp;
+      out.serving[idx] = -1;
+      out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
+                                 0.f, 0.f);
+      if (out.rate64) out.rate64[idx] = 0.0;
+      if (out.util64) out.util64[idx] = 0.0;
+    }
+    if (u == 0) {
+      uint64_t* pw = st.pcg + (size_t)6 * e;
+      *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+      st.t[e] = 0;
+      out.reward[e] = 0.f;
+      out.done[e] = 0;
+      if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    return;
+  }
+
+  const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
+                      (kp.first_step_active || t != 0);
+  const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
+  for (int i = u; i < nb; i += blockDim.x) lds_cnt[i] = 0;
+
+  // ---- 1. movement: workgroup exclusive scan of "needs waypoint" in ue_id order -------
+  const bool need = active && wp.x < 0;
+  const uint64_t mneed = __ballot(need);
+  const uint64_t mact = __ballot(active);
+  if (lane == 0) {
+    lds_wtot[0][w] = __popcll(mneed);
+    lds_wtot[1][w] = __popcll(mact);
+  }
+  __syncthreads();
+  int pre_need = 0, tot_need = 0, pre_act = 0, tot_act = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int cn = lds_wtot[0][i], ca = lds_wtot[1][i];
+    if (i < w) { pre_need += cn; pre_act += ca; }
+    tot_need += cn;
+    tot_act += ca;
+  }
+  if (need) {
+    u128 su = pcg_advance(s, inc, 2 * (pre_need + __popcll(mneed & lt)), tb.jump);
+    wp.x = pcg_draw_coord(su, inc, kp.Wd);
+    wp.y = pcg_draw_coord(su, inc, kp.Hd);
+  }
+  if (active) move_ue(pos, wp, kp.vel);
+
+  // ---- 2. association (BS coordinates are workgroup-uniform: scalar loads) ------------
+  unsigned best = UINT_MAX;
+  if (active) {
+    const int2* bs = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+#pragma unroll 8
+    for (int b = 0; b < nb; ++b) {
+      const int2 p = bs[b];
+      const int ddx = pos.x - p.x;
+      const int ddy = pos.y - p.y;
+      const unsigned key = ((unsigned)(ddx * ddx + ddy * ddy) << kKeyBits) | (unsigned)b;
+      best = min(best, key);
+    }
+  }
+  const int d2s = (int)(best >> kKeyBits);
+  const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+
+  // ---- 3. per-BS counts via LDS atomics ---------------------------------------------
+  if (srv >= 0) atomicAdd(&lds_cnt[srv], 1);
+  const uint64_t mcon = __ballot(srv >= 0);
+  if (lane == 0) lds_wtot[2][w] = __popcll(mcon);
+  __syncthreads();
+  int pre_con = 0, tot_con = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int cc = lds_wtot[2][i];
+    if (i < w) pre_con += cc;
+    tot_con += cc;
+  }
+
+  // ---- 4. rate + utility -------------------------------------------------------------
+  double rate = 0.0;
+  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], lds_cnt[srv]);
+  const double util = active ? scaled_utility(rate, kp) : 0.0;
+  if (active) lds_util[pre_act + __popcll(mact & lt)] = util;
+  const bool want_metrics = out.metrics != nullptr;
+  if (want_metrics && srv >= 0) lds_rate[pre_con + __popcll(mcon & lt)] = rate;
+  __syncthreads();
+
+  if (valid) {
+    st.ue_xy[idx] = pos;
+    st.wp_xy[idx] = wp;
+    out.serving[idx] = srv;
+    out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
+                               (float)rate, (float)util);
+    if (out.rate64) out.rate64[idx] = rate;
+    if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
+  }
+  if (u == 0) {
+    const double mean_u = tot_act > 0 ? pairwise_any(lds_util, tot_act) / (double)tot_act : kp.lower;
+    const u128 s_next = pcg_advance(s, inc, 2 * tot_need, tb.jump);
+    uint64_t* pw = st.pcg + (size_t)6 * e;
+    *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
+    st.t[e] = t + 1;
+    out.reward[e] = (float)mean_u;
+    out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
+    if (want_metrics) {
+      const double mean_r = tot_con > 0 ? pairwise_any(lds_rate, tot_con) / (double)tot_con : 0.0;
+      out.metrics[e] = make_float4((float)tot_con, (float)tot_con, (float)mean_u, (float)mean_r);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Table builders (run once per context, on the device)
+// ------------------------------------------------------------------------------------
+struct ChanParams {
+  double bw, freq, tx, hb, hu, noise, snr_tr;
+};
+
+// Channel.calculateSNR + Channel.datarate at integer squared distance d2
+// (channels.py:24-27,78-83; OkumuraHata.power_loss channels.py:133-146, same op order).
+__global__ void k_channel_table(ChanParams c, int d2_hi, double* __restrict__ rate,
+                                int* __restrict__ d2max_out, int* __restrict__ count_out) {
+  const int d2 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d2 > d2_hi) return;
+  const double distance = sqrt((double)d2);
+  const double ch = 0.8 + (1.1 * log10(c.freq) - 0.7) * c.hu - 1.56 * log10(c.freq);
+  const double tmp_1 = 69.55 - ch + 26.16 * log10(c.freq) - 13.82 * log10(c.hb);
+  const double tmp_2 = 44.9 - 6.55 * log10(c.hb);
+  const double loss = tmp_1 + tmp_2 * log10(distance + 1e-16);
+  const double power = pow(10.0, (c.tx - loss) / 10.0);
+  const double snr = power / c.noise;
+  const bool conn = snr > c.snr_tr;
+  rate[d2] = conn ? c.bw * log2(1.0 + snr) : 0.0;
+  if (conn) {
+    atomicMax(d2max_out, d2);
+    atomicAdd(count_out, 1);
+  }
+}
+
+// Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
+__global__ void k_jump_table(int kmax, u128* __restrict__ jump) {
+  const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k0 > kmax) return;
+  u128 acc_mult = 1, acc_plus = 0;
+  u128 cur_mult = mk128(PCG_MULT_LO, PCG_MULT_HI), cur_plus = 1;
+  unsigned k = (unsigned)k0;
+  while (k) {
+    if (k & 1u) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    k >>= 1;
+  }
+  jump[2 * k0] = acc_mult;
+  jump[2 * k0 + 1] = acc_plus;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+struct mev_ctx {
+  mev_params p;
+  KParams kp;
+  int device;
+  int d2max;
+  int jmax;
+  double* rate_full;
+  u128* jump;
+};
+
+static thread_local char g_hip_err[256] = "";
+
+#define MEV_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (call);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      snprintf(g_hip_err, sizeof(g_hip_err), "%s:%d %s: %s", __FILE__, __LINE__, #call, \
+               hipGetErrorString(_e));                                                 \
+      return MEV_EHIP;                                                                 \
+    }                                                                                  \
+  } while (0)
+
+// Exported functions get C linkage from their declarations in mev.h.
+
+int mev_abi_version(void) { return MEV_ABI_VERSION; }
+
+const char* mev_last_hip_error(void) { return g_hip_err; }
+
+const char* mev_strerror(int code) {
+  switch (code) {
+    case MEV_OK: return "ok";
+    case MEV_EINVAL: return "invalid parameters";
+    case MEV_ENOMEM: return "device allocation failed";
+    case MEV_EHIP: return g_hip_err[0] ? g_hip_err : "HIP runtime error";
+    case MEV_ECHANNEL: return "channel connectivity is not a prefix of the squared distance";
+    default: return "unknown error";
+  }
+}
+
+static int validate(const mev_params* p) {
+  if (!p) return MEV_EINVAL;
+  if (p->num_envs < 1 || p->num_ues < 1 || p->num_ues > kMaxU) return MEV_EINVAL;
+  if (p->num_bs < 1 || p->num_bs > kMaxB) return MEV_EINVAL;
+  if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
+  if (p->ep_max_time < 1 || p->arrival_exit < 1) return MEV_EINVAL;
+  if (!(p->velocity >= 0.0) || !(p->ue_noise > 0.0) || !(p->util_upper > p->util_lower))
+    return MEV_EINVAL;
+  return MEV_OK;
+}
+
+int mev_create(const mev_params* params, mev_ctx** out) {
+  if (!out) return MEV_EINVAL;
+  *out = nullptr;
+  int rc = validate(params);
+  if (rc) return rc;
+  mev_ctx* c = new (std::nothrow) mev_ctx();
+  if (!c) return MEV_ENOMEM;
+  c->p = *params;
+  MEV_HIP(hipGetDevice(&c->device));
+
+  // ---- channel table on the device ----
+  const int d2_hi = (params->width - 1) * (params->width - 1) +
+                    (params->height - 1) * (params->height - 1);
+  int* d_aux = nullptr;
+  if (hipMalloc(&c->rate_full, sizeof(double) * (size_t)(d2_hi + 1)) != hipSuccess ||
+      hipMalloc(&d_aux, 2 * sizeof(int)) != hipSuccess) {
+    delete c;
+    return MEV_ENOMEM;
+  }
+  const int init_aux[2] = {-1, 0};
+  MEV_HIP(hipMemcpy(d_aux, init_aux, sizeof(init_aux), hipMemcpyHostToDevice));
+  ChanParams cp{params->bs_bw, params->bs_freq, params->bs_tx, params->bs_height,
+                params->ue_height, params->ue_noise, params->ue_snr_tr};
+  hipLaunchKernelGGL(k_channel_table, dim3((d2_hi + 256) / 256), dim3(256), 0, 0, cp, d2_hi,
+                     c->rate_full, d_aux, d_aux + 1);
+  MEV_HIP(hipGetLastError());
+  int aux[2];
+  MEV_HIP(hipMemcpy(aux, d_aux, sizeof(aux), hipMemcpyDeviceToHost));
+  MEV_HIP(hipFree(d_aux));
+  c->d2max = aux[0];
+  if (aux[1] != aux[0] + 1) {  // connectable set must be exactly [0, d2max]
+    (void)hipFree(c->rate_full);
+    delete c;
+    return MEV_ECHANNEL;
+  }
+
+  // ---- PCG64 jump table: offsets up to 2U (reset) + 2U (waypoints) ----
+  c->jmax = 4 * params->num_ues;
+  if (hipMalloc(&c->jump, sizeof(u128) * 2 * (size_t)(c->jmax + 1)) != hipSuccess) {
+    (void)hipFree(c->rate_full);
+    delete c;
+    return MEV_ENOMEM;
+  }
+  hipLaunchKernelGGL(k_jump_table, dim3((c->jmax + 256) / 256), dim3(256), 0, 0, c->jmax,
+                     c->jump);
+  MEV_HIP(hipGetLastError());
+  MEV_HIP(hipDeviceSynchronize());
+
+  KParams& kp = c->kp;
+  kp.E = params->num_envs;
+  kp.U = params->num_ues;
+  kp.B = params->num_bs;
+  kp.W = params->width;
+  kp.H = params->height;
+  kp.t_end = params->ep_max_time < params->arrival_exit ? params->ep_max_time
+                                                         : params->arrival_exit;
+  kp.arr_start = params->arrival_start;
+  kp.arr_exit = params->arrival_exit;
+  kp.first_step_active = params->first_step_active;
+  kp.movement_reseed = params->movement_reseed;
+  kp.d2max = c->d2max;
+  kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
+  kp.Wd = (double)params->width;
+  kp.Hd = (double)params->height;
+  kp.vel = params->velocity;
+  kp.lower = params->util_lower;
+  kp.upper = params->util_upper;
+  kp.w1 = params->util_w1;
+  kp.w2 = params->util_w2;
+  kp.log_w3 = log(params->util_w3);
+  *out = c;
+  return MEV_OK;
+}
+
+void mev_destroy(mev_ctx* c) {
+  if (!c) return;
+  (void)hipFree(c->rate_full);
+  (void)hipFree(c->jump);
+  delete c;
+}
+
+int mev_d2max(const mev_ctx* c) { return c ? c->d2max : MEV_EINVAL; }
+
+const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
+
+int mev_copy_rate_table(const mev_ctx* c, double* dst, int64_t n) {
+  if (!c || !dst || n < 0 || n > (int64_t)c->d2max + 1) return MEV_EINVAL;
+  MEV_HIP(hipMemcpy(dst, c->rate_full, sizeof(double) * (size_t)n, hipMemcpyDefault));
+  return MEV_OK;
+}
+
+static int check_bufs(const mev_ctx* c, const mev_state* st, const mev_outputs* out) {
+  if (!c || !st || !out) return MEV_EINVAL;
+  if (!st->ue_xy || !st->wp_xy || !st->pcg || !st->t || !st->bs_xy) return MEV_EINVAL;
+  if (!out->obs || !out->serving || !out->reward || !out->done) return MEV_EINVAL;
+  return MEV_OK;
+}
+
+static void to_kernel(const mev_state* st, const mev_outputs* out, KState& ks, KOut& ko) {
+  ks.ue_xy = reinterpret_cast<int2*>(st->ue_xy);
+  ks.wp_xy = reinterpret_cast<int2*>(st->wp_xy);
+  ks.pcg = st->pcg;
+  ks.t = st->t;
+  ks.bs_xy = reinterpret_cast<const int2*>(st->bs_xy);
+  ks.bs_count = st->bs_count;
+  ko.obs = reinterpret_cast<float4*>(out->obs);
+  ko.serving = out->serving;
+  ko.reward = out->reward;
+  ko.done = out->done;
+  ko.rate64 = out->rate64;
+  ko.util64 = out->util64;
+  ko.metrics = reinterpret_cast<float4*>(out->metrics);
+}
+
+template <bool RESET>
+static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
+                  const uint8_t* mask, hipStream_t stream) {
+  KState ks;
+  KOut ko;
+  to_kernel(st, out, ks, ko);
+  KTables tb{c->rate_full, c->jump};
+  const KParams& kp = c->kp;
+  const bool per_env = c->p.bs_per_env != 0;
+  if (kp.U <= 64) {
+    const long waves = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
+    const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+    if (per_env)
+      hipLaunchKernelGGL((k_step_packed<true, RESET>), grid, dim3(kPackedBlock), 0, stream, kp,
+                         ks, ko, tb, mask);
+    else
+      hipLaunchKernelGGL((k_step_packed<false, RESET>), grid, dim3(kPackedBlock), 0, stream, kp,
+                         ks, ko, tb, mask);
+  } else {
+    const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
+    if (per_env)
+      hipLaunchKernelGGL((k_step_block<true, RESET>), dim3(kp.E), block, 0, stream, kp, ks, ko,
+                         tb, mask);
+    else
+      hipLaunchKernelGGL((k_step_block<false, RESET>), dim3(kp.E), block, 0, stream, kp, ks, ko,
+                         tb, mask);
+  }
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
+int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
+              const uint8_t* env_mask, void* stream) {
+  int rc = check_bufs(c, st, out);
+  if (rc) return rc;
+  return launch<true>(c, st, out, env_mask, (hipStream_t)stream);
+}
+
+int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int32_t nsteps,
+             void* stream) {
+  int rc = check_bufs(c, st, out);
+  if (rc) return rc;
+  if (nsteps < 0) return MEV_EINVAL;
+  for (int i = 0; i < nsteps; ++i) {
+    rc = launch<false>(c, st, out, nullptr, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return MEV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// numpy-compatible seeding (host): SeedSequence(seed).generate_state(4, uint64) ->
+// PCG64 srandom (numpy/random/bit_generator.pyx, numpy/random/src/pcg64/pcg64.c).
+// --------------------------------------------------------------------------------------
+static uint32_t ss_hashmix(uint32_t value, uint32_t* hash_const) {
+  value ^= *hash_const;
+  *hash_const *= 0x931e8875u;  // MULT_A
+  value *= *hash_const;
+  value ^= value >> 16;
+  return value;
+}
+
+static uint32_t ss_mix(uint32_t x, uint32_t y) {
+  uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;  // MIX_MULT_L, MIX_MULT_R
+  r ^= r >> 16;
+  return r;
+}
+
+static void seed_sequence_state(uint64_t seed, uint64_t out_words[4]) {
+  uint32_t entropy[2];
+  int n_ent = 0;
+  uint64_t v = seed;
+  do {  // _coerce_to_uint32_array: little-endian 32-bit words, at least one
+    entropy[n_ent++] = (uint32_t)(v & 0xffffffffu);
+    v >>= 32;
+  } while (v && n_ent < 2);
+  uint32_t pool[4];
+  uint32_t hc = 0x43b0d7e5u;  // INIT_A
+  for (int i = 0; i < 4; ++i) pool[i] = ss_hashmix(i < n_ent ? entropy[i] : 0u, &hc);
+  for (int src = 0; src < 4; ++src)
+    for (int dst = 0; dst < 4; ++dst)
+      if (src != dst) pool[dst] = ss_mix(pool[dst], ss_hashmix(pool[src], &hc));
+  for (int src = 4; src < n_ent; ++src)
+    for (int dst = 0; dst < 4; ++dst) pool[dst] = ss_mix(pool[dst], ss_hashmix(entropy[src], &hc));
+  uint32_t st32[8];
+  uint32_t hb = 0x8b51f9ddu;  // INIT_B
+  for (int i = 0; i < 8; ++i) {
+    uint32_t d = pool[i % 4];
+    d ^= hb;
+    hb *= 0x58f38dedu;  // MULT_B
+    d *= hb;
+    d ^= d >> 16;
+    st32[i] = d;
+  }
+  for (int i = 0; i < 4; ++i) out_words[i] = (uint64_t)st32[2 * i] | ((uint64_t)st32[2 * i + 1] << 32);
+}
+
+int mev_seed_pcg64(const uint64_t* seeds, int64_t n, uint64_t* rows) {
+  if ((!seeds || !rows) && n > 0) return MEV_EINVAL;
+  const u128 mult = ((u128)PCG_MULT_HI << 64) | PCG_MULT_LO;
+  for (int64_t i = 0; i < n; ++i) {
+    if (seeds[i] >> 63) return MEV_EINVAL;
+    uint64_t w[4];
+    seed_sequence_state(seeds[i], w);
+    // pcg64_set_seed: initstate = (w0 << 64) | w1, initseq = (w2 << 64) | w3
+    const u128 initstate = ((u128)w[0] << 64) | w[1];
+    const u128 initseq = ((u128)w[2] << 64) | w[3];
+    const u128 inc = (initseq << 1) | 1;
+    u128 s = 0;
+    s = s * mult + inc;
+    s += initstate;
+    s = s * mult + inc;
+    uint64_t* r = rows + 6 * i;
+    r[0] = (uint64_t)s;
+    r[1] = (uint64_t)(s >> 64);
+    r[2] = (uint64_t)inc;
+    r[3] = (uint64_t)(inc >> 64);
+    r[4] = r[0];
+    r[5] = r[1];
+  }
+  return MEV_OK;
+}
+

@@ -1,0 +1,120 @@
+"""ctypes binding of libmev.so -- the C ABI declared in include/mev.h.
+
+The library is built in-tree by ``make -C mobile-env-gan_amd/csrc`` (or
+``__graft_entry__.build()``) into ``mobile-env-gan_amd/lib/libmev.so``. There is no CPU
+fallback: if the library is missing or fails to load, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
+
+ABI_VERSION = 1
+MEV_OK = 0
+MEV_EINVAL = -22
+MEV_ENOMEM = -12
+MEV_EHIP = -1000
+MEV_ECHANNEL = -1001
+
+# every symbol include/mev.h declares (tests check the library exports all of them)
+EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_rate_table",
+           "mev_copy_rate_table", "mev_seed_pcg64", "mev_reset", "mev_step", "mev_strerror", "mev_last_hip_error")
+
+
+class MevParams(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("num_ues", C.c_int32), ("num_bs", C.c_int32),
+        ("width", C.c_int32), ("height", C.c_int32), ("ep_max_time", C.c_int32),
+        ("arrival_start", C.c_int32), ("arrival_exit", C.c_int32),
+        ("bs_per_env", C.c_int32), ("first_step_active", C.c_int32),
+        ("movement_reseed", C.c_int32),
+        ("velocity", C.c_double),
+        ("bs_bw", C.c_double), ("bs_freq", C.c_double), ("bs_tx", C.c_double),
+        ("bs_height", C.c_double),
+        ("ue_snr_tr", C.c_double), ("ue_noise", C.c_double), ("ue_height", C.c_double),
+        ("util_lower", C.c_double), ("util_upper", C.c_double),
+        ("util_w1", C.c_double), ("util_w2", C.c_double), ("util_w3", C.c_double),
+    ]
+
+
+class MevState(C.Structure):
+    _fields_ = [("ue_xy", C.c_void_p), ("wp_xy", C.c_void_p), ("pcg", C.c_void_p),
+                ("t", C.c_void_p), ("bs_xy", C.c_void_p), ("bs_count", C.c_void_p)]
+
+
+class MevOutputs(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("serving", C.c_void_p), ("reward", C.c_void_p),
+                ("done", C.c_void_p), ("rate64", C.c_void_p), ("util64", C.c_void_p),
+                ("metrics", C.c_void_p)]
+
+
+class MevError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        msg = lib().mev_strerror(code).decode(errors="replace") if _LIB else str(code)
+        super().__init__(f"{where} failed ({code}): {msg}")
+
+
+_LIB = None
+_LOCK = threading.Lock()
+
+
+def lib():
+    """Load libmev.so once; raise loudly if it is absent (no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libmev.so not found at {LIB_PATH}: build it with `make -C mobile-env-gan_amd/csrc`"
+                " or __graft_entry__.build() -- the engine has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        L.mev_abi_version.restype = C.c_int
+        L.mev_create.argtypes = [C.POINTER(MevParams), C.POINTER(C.c_void_p)]
+        L.mev_create.restype = C.c_int
+        L.mev_destroy.argtypes = [C.c_void_p]
+        L.mev_destroy.restype = None
+        L.mev_d2max.argtypes = [C.c_void_p]
+        L.mev_d2max.restype = C.c_int
+        L.mev_rate_table.argtypes = [C.c_void_p]
+        L.mev_rate_table.restype = C.c_void_p
+        L.mev_copy_rate_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.mev_copy_rate_table.restype = C.c_int
+        L.mev_seed_pcg64.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+        L.mev_seed_pcg64.restype = C.c_int
+        L.mev_reset.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),
+                                C.c_void_p, C.c_void_p]
+        L.mev_reset.restype = C.c_int
+        L.mev_step.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),
+                               C.c_int32, C.c_void_p]
+        L.mev_step.restype = C.c_int
+        L.mev_strerror.argtypes = [C.c_int]
+        L.mev_strerror.restype = C.c_char_p
+        L.mev_last_hip_error.restype = C.c_char_p
+        if L.mev_abi_version() != ABI_VERSION:
+            raise ImportError(f"libmev ABI {L.mev_abi_version()} != expected {ABI_VERSION}")
+        _LIB = L
+        return L
+
+
+def check(code: int, where: str):
+    if code != MEV_OK:
+        raise MevError(code, where)
+
+
+def seed_pcg64(seeds) -> "list[int]":
+    """numpy-compatible PCG64 seeding (host C): rows of 6 uint64 per seed."""
+    import numpy as np  # host-side buffer only
+
+    s = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64).reshape(-1))
+    rows = np.zeros((len(s), 6), dtype=np.uint64)
+    check(lib().mev_seed_pcg64(s.ctypes.data, len(s), rows.ctypes.data), "mev_seed_pcg64")
+    return rows

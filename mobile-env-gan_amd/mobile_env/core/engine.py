@@ -1,0 +1,201 @@
+"""StepEngine: batched env state as SoA device tensors + the libmev.so kernels.
+
+This is the host side of the hot path. It owns (as torch tensors on one GPU) the state of
+E independent mobile-env instances and drives the fused HIP step kernel through the C ABI
+(include/mev.h). It replaces, for a whole batch at once, the per-object state the
+reference keeps in entity/plugin objects:
+
+=====================  ===================================  ============================
+tensor                 reference state                      reference file:line
+=====================  ===================================  ============================
+``ue_xy [E,U,2] i32``  ``UserEquipment.x/.y``               entities.py:47-48, base.py:233
+``wp_xy [E,U,2] i32``  ``RandomWaypointMovement``           movement.py:33,44-47,55
+                       ``.userMoveDirection`` (x<0: none)
+``pcg [E,6] u64``      ``Movement.rng`` (numpy PCG64)       movement.py:16-18
+``t [E] i32``          ``MComCore.time``                    base.py:175,280
+``bs_xy [B,2]/[E,B,2]`` ``BaseStation.x/.y`` (int-truncated) entities.py:18,24-26
+=====================  ===================================  ============================
+
+Outputs per step: ``obs [E,U,4] f32`` = (x/W, y/H, data rate, scaled utility),
+``serving [E,U] i32``, ``reward [E] f32`` (mean utility, metrics.py:25-28), ``done [E] u8``,
+and optionally ``rate64``/``util64 [E,U] f64`` and ``metrics [E,4] f32``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _native as N
+
+
+@dataclass
+class EngineParams:
+    """Flattened scenario + plugin parameters (lowered from the MComCore config dict)."""
+    num_envs: int
+    num_ues: int
+    num_bs: int
+    width: int = 200
+    height: int = 200
+    ep_max_time: int = 20
+    arrival_start: int = 0
+    arrival_exit: int = 20
+    first_step_active: bool = True
+    movement_reseed: bool = True
+    velocity: float = 1.5
+    bs: dict = field(default_factory=lambda: {"bw": 9e6, "freq": 2500, "tx": 40, "height": 50})
+    ue: dict = field(default_factory=lambda: {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6})
+    util_lower: float = -20.0
+    util_upper: float = 20.0
+    util_coeffs: tuple = (10.0, 0.0, 10.0)
+
+    def to_c(self, bs_per_env: bool) -> N.MevParams:
+        return N.MevParams(
+            num_envs=self.num_envs, num_ues=self.num_ues, num_bs=self.num_bs,
+            width=int(self.width), height=int(self.height), ep_max_time=int(self.ep_max_time),
+            arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
+            bs_per_env=int(bs_per_env), first_step_active=int(bool(self.first_step_active)),
+            movement_reseed=int(bool(self.movement_reseed)),
+            velocity=float(self.velocity),
+            bs_bw=float(self.bs["bw"]), bs_freq=float(self.bs["freq"]),
+            bs_tx=float(self.bs["tx"]), bs_height=float(self.bs["height"]),
+            ue_snr_tr=float(self.ue["snr_tr"]), ue_noise=float(self.ue["noise"]),
+            ue_height=float(self.ue["height"]),
+            util_lower=float(self.util_lower), util_upper=float(self.util_upper),
+            util_w1=float(self.util_coeffs[0]), util_w2=float(self.util_coeffs[1]),
+            util_w3=float(self.util_coeffs[2]))
+
+    @property
+    def t_end(self) -> int:
+        return min(int(self.ep_max_time), int(self.arrival_exit))
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(None)
+
+
+class StepEngine:
+    """E envs on one GPU. ``seeds`` are config seeds (movement stream = seed + 4,
+    base.py:156-168); ``bs_xy`` is [B,2] (shared layout) or [E,B,2] (+ ``bs_count`` [E])."""
+
+    def __init__(self, params: EngineParams, bs_xy, seeds, bs_count=None, device=None,
+                 rate64: bool = False, util64: bool = False, metrics: bool = False):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("StepEngine runs on a ROCm GPU only (no CPU fallback)")
+        self.device = device
+        self.p = params
+        E, U = params.num_envs, params.num_ues
+        bs = torch.as_tensor(bs_xy, dtype=torch.int32)
+        self.bs_per_env = bs.dim() == 3
+        if self.bs_per_env:
+            if bs.shape[0] != E or bs.shape[2] != 2:
+                raise ValueError(f"bs_xy must be [E,B,2], got {tuple(bs.shape)}")
+        elif bs.dim() != 2 or bs.shape[1] != 2:
+            raise ValueError(f"bs_xy must be [B,2] or [E,B,2], got {tuple(bs.shape)}")
+        B = bs.shape[-2]
+        if B != params.num_bs:
+            raise ValueError(f"bs_xy has {B} stations, params say {params.num_bs}")
+        L = N.lib()
+        with torch.cuda.device(device):
+            cp = params.to_c(self.bs_per_env)
+            ctx = C.c_void_p()
+            N.check(L.mev_create(C.byref(cp), C.byref(ctx)), "mev_create")
+            self._ctx = ctx
+            self._lib = L
+            kw = dict(device=device)
+            self.bs_xy = bs.contiguous().to(**kw)
+            self.bs_count = None
+            if bs_count is not None:
+                self.bs_count = torch.as_tensor(bs_count, dtype=torch.int32).reshape(E).to(**kw)
+                if int(self.bs_count.max()) > B or int(self.bs_count.min()) < 0:
+                    raise ValueError("bs_count out of range")
+            self.ue_xy = torch.zeros((E, U, 2), dtype=torch.int32, **kw)
+            self.wp_xy = torch.full((E, U, 2), -1, dtype=torch.int32, **kw)
+            self.t = torch.full((E,), params.t_end, dtype=torch.int32, **kw)
+            self.pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
+            self.obs = torch.zeros((E, U, 4), dtype=torch.float32, **kw)
+            self.serving = torch.full((E, U), -1, dtype=torch.int32, **kw)
+            self.reward = torch.zeros((E,), dtype=torch.float32, **kw)
+            self.done = torch.zeros((E,), dtype=torch.uint8, **kw)
+            self.rate64 = torch.zeros((E, U), dtype=torch.float64, **kw) if rate64 else None
+            self.util64 = torch.zeros((E, U), dtype=torch.float64, **kw) if util64 else None
+            self.metrics = torch.zeros((E, 4), dtype=torch.float32, **kw) if metrics else None
+        self.seed(seeds)
+        self._bind()
+
+    # -- plumbing -----------------------------------------------------------------------------
+    def _bind(self):
+        self._st = N.MevState(_ptr(self.ue_xy), _ptr(self.wp_xy), _ptr(self.pcg), _ptr(self.t),
+                              _ptr(self.bs_xy), _ptr(self.bs_count))
+        self._out = N.MevOutputs(_ptr(self.obs), _ptr(self.serving), _ptr(self.reward),
+                                 _ptr(self.done), _ptr(self.rate64), _ptr(self.util64),
+                                 _ptr(self.metrics))
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def d2max(self) -> int:
+        return int(self._lib.mev_d2max(self._ctx))
+
+    def rate_table(self):
+        """Host copy (numpy float64) of the device-built channel table rate_full[0..d2max]."""
+        import numpy as np
+        host = np.zeros(self.d2max + 1, dtype=np.float64)
+        N.check(self._lib.mev_copy_rate_table(self._ctx, host.ctypes.data, len(host)),
+                "mev_copy_rate_table")
+        return host
+
+    # -- API ----------------------------------------------------------------------------------
+    def seed(self, seeds):
+        """Set per-env config seeds (movement stream = seed + 4); takes effect at reset."""
+        import numpy as np
+        s = np.asarray(seeds, dtype=np.int64).reshape(-1)
+        if len(s) == 1 and self.p.num_envs > 1:
+            s = s[0] + np.arange(self.p.num_envs, dtype=np.int64)
+        if len(s) != self.p.num_envs:
+            raise ValueError(f"need {self.p.num_envs} seeds, got {len(s)}")
+        rows = N.seed_pcg64((s + 4).astype(np.uint64))
+        self.pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
+        self.t.fill_(self.p.t_end)
+
+    def set_bs_layout(self, bs_xy, bs_count=None):
+        bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)
+        if tuple(bs.shape) != tuple(self.bs_xy.shape):
+            raise ValueError("layout shape mismatch")
+        self.bs_xy.copy_(bs)
+        if bs_count is not None:
+            if self.bs_count is None:
+                raise ValueError("engine was built without bs_count")
+            self.bs_count.copy_(torch.as_tensor(bs_count, dtype=torch.int32))
+
+    def reset(self, mask=None):
+        """MComCore.reset for all envs (mask None) or envs where mask[e] != 0."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_reset(self._ctx, C.byref(self._st), C.byref(self._out),
+                                        _ptr(m), self._stream()), "mev_reset")
+        self._keep = m  # keep mask alive until the launch is consumed
+
+    def step(self, nsteps: int = 1):
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_step(self._ctx, C.byref(self._st), C.byref(self._out),
+                                       int(nsteps), self._stream()), "mev_step")
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            torch.cuda.synchronize(self.device)
+            self._lib.mev_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,295 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE implementation.
+
+Runs ONLY in the development container, where the read-only reference checkout exists at
+/root/reference. Nothing on the GPU box runs this script; the tests there read the committed
+.npz/.json files it produced. The reference package is imported (never copied) with three
+stub modules for its render-only / geometry dependencies that are absent from the image:
+
+* ``pygame``            -- rendering only (reference base.py:12,15)
+* ``shapely.geometry``  -- ``Point(x, y).distance`` = sqrt(dx^2 + dy^2) on the integer
+                           coordinates produced by entities.py:24-26,52-54 (GEOS computes the
+                           same IEEE value for integer inputs; validated by the two notebook
+                           snapshots, which the reference reproduces bit-for-bit with this stub)
+* ``svgpath2mpl``       -- BS glyph for rendering only (reference util.py:4,24)
+
+The per-step JSON dump of the reference (base.py:261,298-349) is disabled and the process runs
+from a scratch directory. Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import random
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+LAYOUTS = os.path.join(HERE, "..", "..", "mobile-env-gan_amd", "mobile_env", "scenarios",
+                       "layouts.json")
+METRIC_NAMES = ["number connections", "number connected", "mean utility", "mean datarate"]
+
+
+def _install_stubs():
+    import matplotlib
+    matplotlib.use("Agg")
+    from matplotlib.path import Path
+
+    pg = types.ModuleType("pygame")
+    pg.Surface = object
+    sys.modules["pygame"] = pg
+
+    class Point:
+        def __init__(self, x, y):
+            self.x = float(x)
+            self.y = float(y)
+
+        def distance(self, other):
+            dx = self.x - other.x
+            dy = self.y - other.y
+            return math.sqrt(dx * dx + dy * dy)
+
+    shp = types.ModuleType("shapely")
+    geom = types.ModuleType("shapely.geometry")
+    geom.Point = Point
+    shp.geometry = geom
+    sys.modules["shapely"] = shp
+    sys.modules["shapely.geometry"] = geom
+
+    svg = types.ModuleType("svgpath2mpl")
+    svg.parse_path = lambda s: Path(np.zeros((3, 2)))
+    sys.modules["svgpath2mpl"] = svg
+
+
+def _import_reference():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    from mobile_env.core import base as ref_base  # noqa: E402
+    from mobile_env.core.entities import BaseStation, UserEquipment  # noqa: E402
+    from mobile_env.core.channels import OkumuraHata  # noqa: E402
+    from mobile_env.scenarios import custom as ref_custom  # noqa: E402
+
+    # disable per-step disk dump (base.py:261)
+    ref_base.MComCore.save_layout_and_data_rates = lambda self, e, s: None
+    return ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom
+
+
+def _record_step(env, users):
+    """Snapshot the reference env state after one step() call."""
+    U = len(users)
+    xy = np.array([[int(ue.x), int(ue.y)] for ue in users], dtype=np.int64)
+    serving = np.full(U, -1, dtype=np.int64)
+    for (bs, ue) in env.bs2ue_dataRates.keys():
+        serving[ue.ue_id] = bs.bs_id
+    rate = np.array([float(env.allUserDataRates.get(ue, 0.0)) for ue in users])
+    util = np.array([float(env.ue_utilities[ue]) if ue in env.ue_utilities else np.nan
+                     for ue in users])
+    met = np.array([float(env.monitor.scalar_results[n][-1]) for n in METRIC_NAMES])
+    return xy, serving, rate, util, met
+
+
+def _make_fixed_core(ref_base, BaseStation, UserEquipment):
+    class FixedCore(ref_base.MComCore):
+        """MComCore over a fixed station list, with the episode bookkeeping that the only
+        runnable scenario performs after reset (custom.py:53-62): activeUsers = UEs with
+        startTime <= 0 sorted by id, and the history lists initialised."""
+
+        def reset(self, *, seed=None):
+            super().reset(seed=seed)
+            self.activeUsers = sorted(
+                [ue for ue in self.userDict.values() if ue.startTime <= 0],
+                key=lambda ue: ue.ue_id)
+            self.users_dataRateList = {ue.ue_id: [] for ue in self.userDict.values()}
+            self.users_trajectoryList = {ue.ue_id: [] for ue in self.userDict.values()}
+
+    def build(bs_xy, num_ues, seed, bs_params=None, ue_params=None, extra=None):
+        cfg = FixedCore.default_config()
+        if bs_params:
+            cfg["bs"].update(bs_params)
+        if ue_params:
+            cfg["ue"].update(ue_params)
+        stations = [BaseStation(i, (int(x), int(y)), **cfg["bs"]) for i, (x, y) in enumerate(bs_xy)]
+        users = [UserEquipment(i, **cfg["ue"]) for i in range(num_ues)]
+        config = {"seed": seed, "bs": cfg["bs"], "ue": cfg["ue"]}
+        if extra:
+            config.update(extra)
+        return FixedCore(stations, users, config), users
+
+    return build
+
+
+def run_episodes(env, users, episodes, steps):
+    """collectData2.ipynb driver loop: reset(); step(epoch, s) for s in range(steps)."""
+    rec = {k: [] for k in ("init_xy", "xy", "serving", "rate", "util", "metrics")}
+    for ep in range(episodes):
+        env.reset()
+        rec["init_xy"].append([[int(ue.x), int(ue.y)] for ue in users])
+        for s in range(steps):
+            env.step(ep, s)
+            xy, srv, rate, util, met = _record_step(env, users)
+            rec["xy"].append(xy)
+            rec["serving"].append(srv)
+            rec["rate"].append(rate)
+            rec["util"].append(util)
+            rec["metrics"].append(met)
+    return {k: np.asarray(v) for k, v in rec.items()}
+
+
+def rate_table(OkumuraHata, bs_params, ue_params, d2_hi):
+    """Reference channel chain evaluated at every integer squared distance d2 in [0, d2_hi]:
+    (snr, datarate) through OkumuraHata.power_loss / Channel.calculateSNR / Channel.datarate
+    (channels.py:24-27,78-83,133-146), using duck-typed entities whose point distance is
+    sqrt(d2)."""
+
+    class _P:
+        def __init__(self, d2):
+            self.d2 = d2
+
+        def distance(self, other):
+            return math.sqrt(other.d2)
+
+    class _BS:
+        point = _P(0)
+        bw = bs_params["bw"]
+        frequency = bs_params["freq"]
+        tx_power = bs_params["tx"]
+        height = bs_params["height"]
+
+    class _UE:
+        height = ue_params["height"]
+        noise = ue_params["noise"]
+        snr_threshold = ue_params["snr_tr"]
+
+    ch = OkumuraHata()
+    ue = _UE()
+    snr = np.empty(d2_hi + 1)
+    rate = np.empty(d2_hi + 1)
+    for d2 in range(d2_hi + 1):
+        ue.point = _P(d2)
+        s = ch.calculateSNR(_BS, ue)
+        snr[d2] = float(s)
+        rate[d2] = float(ch.datarate(_BS, ue, s))
+    return snr, rate
+
+
+def main():
+    ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
+    scratch = tempfile.mkdtemp(prefix="mev_golden_")
+    os.chdir(scratch)
+    build = _make_fixed_core(ref_base, BaseStation, UserEquipment)
+    layouts = json.load(open(LAYOUTS))
+    defaults = ref_base.MComCore.default_config()
+    out = {}
+
+    # -- fixed-layout scenarios (build-defined layouts), several config seeds, 2 episodes ----------
+    plans = [
+        ("small", None, [2024, 7, 123]),
+        ("medium", None, [2024, 11]),
+        ("large", None, [2024, 99]),
+        ("small_v10", ("small", 10), [5, 2024]),
+        ("large_v10", ("large", 10), [31]),
+    ]
+    for name, variant, seeds in plans:
+        base_name, vel = variant if variant else (name, None)
+        lay = layouts[base_name]
+        runs = []
+        for seed in seeds:
+            ue_p = {"velocity": vel} if vel is not None else None
+            env, users = build(lay["bs"], lay["num_ues"], seed, ue_params=ue_p)
+            runs.append(run_episodes(env, users, episodes=2, steps=20))
+        out[name] = dict(
+            bs_xy=np.asarray(lay["bs"], dtype=np.int64),
+            seeds=np.asarray(seeds, dtype=np.int64),
+            velocity=np.float64(vel if vel is not None else defaults["ue"]["velocity"]),
+            **{k: np.stack([r[k] for r in runs]) for k in runs[0]},
+        )
+
+    # -- MComCustom (custom.py) with the global `random` seeded: BS layout redrawn per reset -------
+    runs, bs_layouts = [], []
+    for k in range(8):
+        random.seed(k)
+        env = ref_custom.MComCustom()
+        users = [env.userDict[i] for i in sorted(env.userDict)]
+        rec = {n: [] for n in ("init_xy", "xy", "serving", "rate", "util", "metrics")}
+        lay_k = []
+        for ep in range(2):
+            env.reset()
+            lay_k.append([[int(bs.point.x), int(bs.point.y)] for bs in env.stationDict.values()])
+            rec["init_xy"].append([[int(ue.x), int(ue.y)] for ue in users])
+            for s in range(20):
+                env.step(ep, s)
+                xy, srv, rate, util, met = _record_step(env, users)
+                for n, v in zip(("xy", "serving", "rate", "util", "metrics"),
+                                (xy, srv, rate, util, met)):
+                    rec[n].append(v)
+        runs.append({n: np.asarray(v) for n, v in rec.items()})
+        bs_layouts.append(lay_k)
+    # ragged BS counts (5..10): pad with -1
+    bs_pad = np.full((8, 2, 10, 2), -1, dtype=np.int64)
+    bs_cnt = np.zeros((8, 2), dtype=np.int64)
+    for k, lay_k in enumerate(bs_layouts):
+        for ep, lay in enumerate(lay_k):
+            bs_pad[k, ep, :len(lay)] = lay
+            bs_cnt[k, ep] = len(lay)
+    out["mcom_custom"] = dict(bs_xy=bs_pad, bs_count=bs_cnt, random_seeds=np.arange(8),
+                              seeds=np.full(8, defaults["seed"]), velocity=np.float64(10),
+                              **{k: np.stack([r[k] for r in runs]) for k in runs[0]})
+
+    # -- custom 128 BS x 1024 UE, velocity 10, 3 steps (reference: ~1.5 s/step) --------------------
+    bs128 = np.random.default_rng(0).integers(0, 200, size=(128, 2))
+    env, users = build(bs128.tolist(), 1024, 2024, ue_params={"velocity": 10})
+    env.reset()
+    init = [[int(ue.x), int(ue.y)] for ue in users]
+    recs = []
+    for s in range(3):
+        env.step(0, s)
+        recs.append(_record_step(env, users))
+    out["custom128x1024"] = dict(
+        bs_xy=bs128.astype(np.int64), seeds=np.asarray([2024]), velocity=np.float64(10),
+        init_xy=np.asarray([[init]]),
+        **{k: np.asarray([[r[i] for r in recs]])
+           for i, k in enumerate(("xy", "serving", "rate", "util", "metrics"))})
+
+    # -- notebook snapshots (GNN.ipynb:86-93 and :909-1047) -----------------------------------------
+    snaps = json.load(open(os.path.join(HERE, "notebook_snapshots.json")))
+    nb_bs = snaps["params"]["bs"]
+    nb_ue = snaps["params"]["ue"]
+    for snap in snaps["snapshots"]:
+        env, users = build(snap["bs_xy"], 7, snaps["params"]["seed"], bs_params=nb_bs,
+                           ue_params=nb_ue)
+        env.reset()
+        for s in range(snap["step"] + 1):
+            env.step(0, s)
+        xy, srv, rate, util, met = _record_step(env, users)
+        assert xy.tolist() == snap["ue_xy"], (snap["source"], xy.tolist())
+        got = {int(u): (int(srv[u]), float(rate[u])) for u in range(7) if srv[u] >= 0}
+        want = {int(e["ue_id"]): (int(e["bs_id"]), float(e["data_rate"])) for e in snap["rates"]}
+        assert got == want, (snap["source"], got, want)
+    print("notebook snapshots reproduced by the reference: OK")
+
+    # -- channel tables: reference snr/datarate at every integer d2 ---------------------------------
+    tables = {}
+    for tag, bsp, uep in (("default", defaults["bs"], defaults["ue"]),
+                          ("notebook", {**defaults["bs"], **nb_bs}, {**defaults["ue"], **nb_ue})):
+        snr, rate = rate_table(OkumuraHata, bsp, uep, 80000)
+        conn = snr > uep["snr_tr"]
+        d2max = int(np.nonzero(conn)[0].max())
+        assert conn[: d2max + 1].all() and not conn[d2max + 1:].any(), "connectivity not a prefix"
+        tables[tag] = dict(d2max=np.int64(d2max), rate=rate[: d2max + 1],
+                           snr_margin=np.float64(np.min(np.abs(snr / uep["snr_tr"] - 1.0))),
+                           bs=json.dumps(bsp), ue=json.dumps(uep))
+        print(tag, "d2max", d2max)
+
+    for name, arrs in out.items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+    for tag, arrs in tables.items():
+        np.savez_compressed(os.path.join(HERE, f"channel_{tag}.npz"), **arrs)
+    print("wrote", sorted(out) + [f"channel_{t}" for t in tables])
+
+
+if __name__ == "__main__":
+    main()
