@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: whole-node env-steps/s of the fused HIP step on mobile-large-central-v0.
+
+Contract (see DESIGN.md "Measurement"):
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+* One step = one launch of the fused step kernel over every env on the GPU (BASELINE.json
+  configs[2]: 65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank
+  owns its own 65,536 independent envs, seeds 1000 + global env index).
+* Timed region: barrier + synchronize, K steps, the single final all-gather of the
+  (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
+  ranks time. Inputs are resident in HBM before timing starts.
+* roofline: algorithmic bytes per launch = E * (54*U + 61) over the kernel's
+  average duration, measured with HIP events recorded around every launch on the stream the
+  kernel runs on. traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
+  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
+* cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
+  bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
+  per core, run before the GPU is touched.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mobile-env-gan_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node), mobile-large-central-v0 at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_env_step(num_ues: int, per_env_bs: bool, num_bs: int) -> int:
+    # SURVEY.md 8d canonical layout: per UE 34 B state r+w + 20 B outputs; per env 61 B
+    return 54 * num_ues + 61 + (8 * num_bs if per_env_bs else 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline: the per-object port of the reference step, one process per core
+# ---------------------------------------------------------------------------------------------
+def _cpu_worker(args):
+    layout, num_ues, seed0, budget_s = args
+    from oracle import port
+    done = 0
+    k = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        core = port.build(layout, num_ues, seed0 + k, 1.5)
+        core.reset()
+        for _ in range(20):
+            core.step()
+            done += 1
+        k += 1
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(budget_s: float, procs: int):
+    from mobile_env.scenarios.registry import LAYOUTS
+    lay = LAYOUTS["large"]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(lay["bs"], lay["num_ues"], 1000 + 100000 * i, budget_s)
+                                     for i in range(procs)])
+    wall = time.perf_counter() - t0
+    steps = sum(r[0] for r in res)
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": (f"oracle/port.py per-object restatement of MComCore.step, "
+                       f"mobile-large-central-v0 (13 BS x 30 UE), {procs} processes x "
+                       f"{budget_s:.0f} s of whole 20-step episodes, seeds 1000+, compute-only "
+                       f"(no JSON dump): {steps} env-steps in {wall:.1f} s")}
+
+
+def load_traffic(workload: str, envs: int):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = d.get(f"{workload}@{envs}")
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--workload", default="mobile-large-central-v0")
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-run", action="store_true",
+                    help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.profile_run):
+        procs = max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(args.cpu_budget, procs)
+
+    import torch
+    import torch.distributed as dist
+
+    import mobile_env
+
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    E = args.envs
+    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=1000 + rank * E)
+    U, B = env.num_ues, env.num_bs
+    per_env_bs = env.engine.bs_per_env
+    env.reset()
+    for _ in range(args.warmup):
+        env.step()
+    torch.cuda.synchronize(device)
+
+    K = args.steps
+    stream = torch.cuda.current_stream(device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    gather = None
+    if world > 1:
+        gather = torch.empty((world, 2, E), dtype=torch.float32, device=device)
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        env.step()
+        ev[k][1].record(stream)
+    if world > 1:  # the one collective: final (reward, done) batch to every rank
+        rd = torch.stack([env.engine.reward, env.engine.done.float()])
+        dist.all_gather_into_tensor(gather, rd)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        value = world * E * K / elapsed
+        bpe = algorithmic_bytes_per_env_step(U, per_env_bs, B)
+        algo_bytes = E * bpe
+        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.workload, E)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded PCG64 streams, build-defined BS layout)",
+            "config": {"workload": args.workload, "envs_per_gpu": E, "global_envs": world * E,
+                       "num_ues": U, "num_bs": B,
+                       "parallelism": f"env-sharded x{world}, no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel_ms": kern_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -55,7 +55,11 @@ struct KParams {
   int movement_reseed;
   int d2max;
   int envs_per_wave;  // packed shape only
-  double Wd, Hd, vel, lower, upper, w1, w2, log_w3;
+  int srv_bits;       // bits of a serving-BS index (ceil(log2(B))), for the ballot match
+  int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
+  int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
+  float inv_w, inv_h; // obs normalisation
+  double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
 };
 
 struct KState {
@@ -80,6 +84,7 @@ struct KOut {
 struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
+  const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
 };
 
 // ------------------------------------------------------------------------------------
@@ -196,10 +201,23 @@ __device__ __forceinline__ double scaled_utility(double rate, const KParams& kp)
   return 2.0 * (ur - kp.lower) / (kp.upper - kp.lower) - 1.0;
 }
 
-// ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435).
-__device__ __forceinline__ double shared_rate(double full, int n) {
+// ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435):
+// rint(share * 100) / 100. Returns the rate; `cents` gets rint(share * 100).
+__device__ __forceinline__ double shared_rate(double full, int n, double& cents) {
   const double share = full / (double)n;
-  return rint(share * 100.0) / 100.0;
+  cents = rint(share * 100.0);
+  return cents / 100.0;
+}
+
+// Scaled utility of a rounded rate. The utility depends on the rate only, and the rate is
+// cents/100 for an integer `cents`, so below the saturation point (rate where the clip at
+// `upper` engages) it is read from a table the device built with scaled_utility() itself
+// (identical values); above it, it is the scaled upper bound.
+__device__ __forceinline__ double utility_of(double rate, double cents, const KParams& kp,
+                                             const double* __restrict__ tab) {
+  if (kp.util_direct) return scaled_utility(rate, kp);
+  if (cents <= (double)kp.util_kmax) return tab[(int)cents];
+  return kp.util_sat;
 }
 
 // ------------------------------------------------------------------------------------
@@ -209,6 +227,48 @@ __device__ __forceinline__ double shared_rate(double full, int n) {
 constexpr int kPackedBlock = 256;
 constexpr int kWavesPerBlock = kPackedBlock / 64;
 
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS written by other lanes of this wavefront becomes visible (no workgroup barrier)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// numpy pairwise sum (n <= 64) of the values `v` of the lanes selected by `mtake` inside one
+// env segment (lanes base..base+U-1), in lane order. The 8 block accumulators live in
+// lanes base..base+7 and are combined by a butterfly that reproduces numpy's
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)). Result valid in lane `base`. Called by all lanes.
+__device__ __forceinline__ double seg_pairwise_sum(double v, bool take, uint64_t mtake,
+                                                   uint64_t lt, int base, int u,
+                                                   double* __restrict__ lds) {
+  const int n = __popcll(mtake);
+  if (take) lds[base + __popcll(mtake & lt)] = v;
+  wave_lds_sync();
+  const int nfull = n - (n & 7);
+  double r = 0.0;
+  if (n >= 8 && u < 8) {
+    r = lds[base + u];
+    for (int i = 8; i < nfull; i += 8) r += lds[base + i + u];
+  }
+  r += __shfl(r, base + (u ^ 1));
+  r += __shfl(r, base + (u ^ 2));
+  r += __shfl(r, base + (u ^ 4));
+  double res = r;
+  if (u == 0) {
+    int i = nfull;
+    if (n < 8) {
+      res = -0.0;
+      i = 0;
+    }
+    for (; i < n; ++i) res += lds[base + i];
+  }
+  return res;
+}
+
+// ------------------------------------------------------------------------------------
+// Packed kernel: U <= 64, floor(64/U) envs per wavefront, one lane per UE.
+// RESET=true: only re-initialise envs (optionally masked), write reset obs.
+// ------------------------------------------------------------------------------------
 template <bool PER_ENV_BS, bool RESET>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb,
@@ -230,48 +290,45 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const uint64_t lt = (1ull << lane) - 1ull;
   const size_t idx = (size_t)e * U + u;
 
+  // all loads first (no load waits on another): env row, then this UE's state
   int t = 0;
   int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
-  u128 s = 0, inc = 0;
-  bool do_reset = false;
+  ulonglong2 pa = make_ulonglong2(0, 0), pb = pa, pc = pa;
+  bool msk = true;
   if (valid) {
-    const uint64_t* pr = st.pcg + (size_t)6 * e;
-    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(pr);
-    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(pr + 2);
-    inc = mk128(b.x, b.y);
+    const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e);
+    pa = pr[0];
+    pb = pr[1];
+    pc = pr[2];
     if (RESET) {
-      do_reset = (mask == nullptr) || mask[e];
+      msk = (mask == nullptr) || mask[e];
     } else {
       t = st.t[e];
-      do_reset = t >= kp.t_end;  // lazy auto-reset at the start of the next step
+      pos = st.ue_xy[idx];
+      wp = st.wp_xy[idx];
     }
-    if (do_reset) {
-      // MComCore.reset (base.py:172-209): movement RNG re-seeded (movement.py:16-18),
-      // initial positions in ue_id order, 2 draws per UE (movement.py:64-72).
-      const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
-      const u128 s0 = kp.movement_reseed ? mk128(c.x, c.y) : mk128(a.x, a.y);
-      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
-      pos.x = pcg_draw_coord(su, inc, kp.Wd);
-      pos.y = pcg_draw_coord(su, inc, kp.Hd);
-      s = pcg_advance(s0, inc, 2 * U, tb.jump);
-      wp = make_int2(-1, -1);
-      t = 0;
-    } else {
-      s = mk128(a.x, a.y);
-      if (!RESET) {
-        pos = st.ue_xy[idx];
-        wp = st.wp_xy[idx];
-      }
-    }
+  }
+  const u128 inc = mk128(pb.x, pb.y);
+  u128 s = mk128(pa.x, pa.y);
+  const bool do_reset = valid && (RESET ? msk : (t >= kp.t_end));
+  if (do_reset) {
+    // MComCore.reset (base.py:172-209): movement RNG re-seeded (movement.py:16-18),
+    // initial positions in ue_id order, 2 draws per UE (movement.py:64-72).
+    const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : s;
+    u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
+    pos.x = pcg_draw_coord(su, inc, kp.Wd);
+    pos.y = pcg_draw_coord(su, inc, kp.Hd);
+    s = pcg_advance(s0, inc, 2 * U, tb.jump);
+    wp = make_int2(-1, -1);
+    t = 0;
   }
 
   if (RESET) {
-    if (valid && do_reset) {
+    if (do_reset) {
       st.ue_xy[idx] = pos;
       st.wp_xy[idx] = wp;
       out.serving[idx] = -1;
-      out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
-                                 0.f, 0.f);
+      out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
       if (out.rate64) out.rate64[idx] = 0.0;
       if (out.util64) out.util64[idx] = 0.0;
       if (u == 0) {
@@ -316,46 +373,41 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const int d2s = (int)(best >> kKeyBits);
   const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
 
-  // ---- 3. per-BS connected counts n_b within the env segment (one ballot per BS in use)
-  int n = 0;
-  {
-    uint64_t pending = __ballot(srv >= 0);
-    while (pending) {
-      const int leader = __ffsll((unsigned long long)pending) - 1;
-      const int b = __shfl(srv, leader);
-      const uint64_t mb = __ballot(srv == b);
-      if (srv == b) n = __popcll(mb & segmask);
-      pending &= ~mb;
-    }
+  // ---- 3. n_b for the own serving BS: lanes of the segment with the same index, found by
+  //         matching the index bit by bit with ballots (no LDS, no atomics) ---------------
+  const uint64_t mcon = __ballot(srv >= 0) & segmask;
+  uint64_t match = mcon;
+  for (int bit = 0; bit < kp.srv_bits; ++bit) {
+    const bool on = (srv >> bit) & 1;
+    const uint64_t mb = __ballot(on);
+    match &= on ? mb : ~mb;
   }
+  const int n = __popcll(match);
 
   // ---- 4. rate + utility -------------------------------------------------------------
-  double rate = 0.0;
-  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], n);
-  const double util = active ? scaled_utility(rate, kp) : 0.0;
+  double rate = 0.0, cents = 0.0;
+  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], n, cents);
+  const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) -----
   const uint64_t mact = __ballot(active) & segmask;
   const int nact = __popcll(mact);
-  if (active) lds_util[wib][base + __popcll(mact & lt)] = util;
-  const uint64_t mcon = __ballot(srv >= 0) & segmask;
-  const int ncon = __popcll(mcon);
+  const double sum_u = seg_pairwise_sum(util, active, mact, lt, base, u, lds_util[wib]);
   const bool want_metrics = out.metrics != nullptr;
-  if (want_metrics && srv >= 0) lds_rate[wib][base + __popcll(mcon & lt)] = rate;
-  __syncthreads();
+  double sum_r = 0.0;
+  if (want_metrics) sum_r = seg_pairwise_sum(rate, srv >= 0, mcon, lt, base, u, lds_rate[wib]);
 
   // ---- 6. stores ---------------------------------------------------------------------
   if (valid) {
     st.ue_xy[idx] = pos;
     st.wp_xy[idx] = wp;
     out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
-                               (float)rate, (float)util);
+    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, (float)rate,
+                               (float)util);
     if (out.rate64) out.rate64[idx] = rate;
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
     if (u == 0) {
-      const double mean_u =
-          nact > 0 ? pairwise_small(&lds_util[wib][base], nact) / (double)nact : kp.lower;
+      const double mean_u = nact > 0 ? sum_u / (double)nact : kp.lower;
       const u128 s_next = pcg_advance(s, inc, 2 * __popcll(mneed), tb.jump);
       uint64_t* pw = st.pcg + (size_t)6 * e;
       *reinterpret_cast<ulonglong2*>(pw) =
@@ -364,8 +416,8 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
       out.reward[e] = (float)mean_u;
       out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
       if (want_metrics) {
-        const double mean_r =
-            ncon > 0 ? pairwise_small(&lds_rate[wib][base], ncon) / (double)ncon : 0.0;
+        const int ncon = __popcll(mcon);
+        const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
         out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
       }
     }
@@ -426,8 +478,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
       st.ue_xy[idx] = pos;
       st.wp_xy[idx] = wp;
       out.serving[idx] = -1;
-      out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
-                                 0.f, 0.f);
+      out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
       if (out.rate64) out.rate64[idx] = 0.0;
       if (out.util64) out.util64[idx] = 0.0;
     }
@@ -499,9 +550,9 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   }
 
   // ---- 4. rate + utility -------------------------------------------------------------
-  double rate = 0.0;
-  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], lds_cnt[srv]);
-  const double util = active ? scaled_utility(rate, kp) : 0.0;
+  double rate = 0.0, cents = 0.0;
+  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], lds_cnt[srv], cents);
+  const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
   if (active) lds_util[pre_act + __popcll(mact & lt)] = util;
   const bool want_metrics = out.metrics != nullptr;
   if (want_metrics && srv >= 0) lds_rate[pre_con + __popcll(mcon & lt)] = rate;
@@ -511,8 +562,8 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     st.ue_xy[idx] = pos;
     st.wp_xy[idx] = wp;
     out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)((double)pos.x / kp.Wd), (float)((double)pos.y / kp.Hd),
-                               (float)rate, (float)util);
+    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, (float)rate,
+                               (float)util);
     if (out.rate64) out.rate64[idx] = rate;
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
   }
@@ -559,6 +610,18 @@ __global__ void k_channel_table(ChanParams c, int d2_hi, double* __restrict__ ra
   }
 }
 
+// Scaled-utility table over rounded rates: tab[k] = scaled_utility(k / 100), evaluated by
+// the same device function the step kernel would use (utilities.py:44-55).
+__global__ void k_util_table(KParams kp, int kmax, double* __restrict__ tab,
+                             int* __restrict__ bad) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > kmax) return;
+  const double rate = (double)k / 100.0;
+  const double v = scaled_utility(rate, kp);
+  tab[k] = v;
+  if (k == kmax && v != kp.util_sat) *bad = 1;  // saturation point must lie inside the table
+}
+
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
 __global__ void k_jump_table(int kmax, u128* __restrict__ jump) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -592,6 +655,7 @@ struct mev_ctx {
   int jmax;
   double* rate_full;
   u128* jump;
+  double* util;
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -644,6 +708,44 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   c->p = *params;
   MEV_HIP(hipGetDevice(&c->device));
 
+  KParams& kp = c->kp;
+  kp.E = params->num_envs;
+  kp.U = params->num_ues;
+  kp.B = params->num_bs;
+  kp.W = params->width;
+  kp.H = params->height;
+  kp.t_end = params->ep_max_time < params->arrival_exit ? params->ep_max_time
+                                                         : params->arrival_exit;
+  kp.arr_start = params->arrival_start;
+  kp.arr_exit = params->arrival_exit;
+  kp.first_step_active = params->first_step_active;
+  kp.movement_reseed = params->movement_reseed;
+  kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
+  kp.Wd = (double)params->width;
+  kp.Hd = (double)params->height;
+  kp.vel = params->velocity;
+  kp.lower = params->util_lower;
+  kp.upper = params->util_upper;
+  kp.w1 = params->util_w1;
+  kp.w2 = params->util_w2;
+  kp.log_w3 = log(params->util_w3);
+  kp.inv_w = 1.0f / (float)params->width;
+  kp.inv_h = 1.0f / (float)params->height;
+  kp.srv_bits = 0;
+  while ((1 << kp.srv_bits) < params->num_bs) ++kp.srv_bits;
+  kp.util_sat = 2.0 * (kp.upper - kp.lower) / (kp.upper - kp.lower) - 1.0;
+  // utility saturation point r_sat = w3^(upper/w1) - w2 (increasing utility only)
+  kp.util_direct = 1;
+  kp.util_kmax = 0;
+  if (kp.w1 > 0.0 && params->util_w3 > 1.0 && kp.w2 >= 0.0) {
+    const double r_sat = exp(kp.upper * kp.log_w3 / kp.w1) - kp.w2;
+    const double kmax = ceil((r_sat > 0.0 ? r_sat : 0.0) * 100.0 * 1.01) + 16.0;
+    if (std::isfinite(kmax) && kmax < (double)(1 << 22)) {
+      kp.util_direct = 0;
+      kp.util_kmax = (int)kmax;
+    }
+  }
+
   // ---- channel table on the device ----
   const int d2_hi = (params->width - 1) * (params->width - 1) +
                     (params->height - 1) * (params->height - 1);
@@ -664,6 +766,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   MEV_HIP(hipMemcpy(aux, d_aux, sizeof(aux), hipMemcpyDeviceToHost));
   MEV_HIP(hipFree(d_aux));
   c->d2max = aux[0];
+  c->kp.d2max = c->d2max;
   if (aux[1] != aux[0] + 1) {  // connectable set must be exactly [0, d2max]
     (void)hipFree(c->rate_full);
     delete c;
@@ -680,30 +783,34 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   hipLaunchKernelGGL(k_jump_table, dim3((c->jmax + 256) / 256), dim3(256), 0, 0, c->jmax,
                      c->jump);
   MEV_HIP(hipGetLastError());
+
+  // ---- utility table over rounded rates ----
+  c->util = nullptr;
+  if (!c->kp.util_direct) {
+    const int kmax = c->kp.util_kmax;
+    int* d_bad = nullptr;
+    if (hipMalloc(&c->util, sizeof(double) * (size_t)(kmax + 1)) != hipSuccess ||
+        hipMalloc(&d_bad, sizeof(int)) != hipSuccess) {
+      (void)hipFree(c->rate_full);
+      (void)hipFree(c->jump);
+      delete c;
+      return MEV_ENOMEM;
+    }
+    MEV_HIP(hipMemset(d_bad, 0, sizeof(int)));
+    hipLaunchKernelGGL(k_util_table, dim3((kmax + 256) / 256), dim3(256), 0, 0, c->kp, kmax,
+                       c->util, d_bad);
+    MEV_HIP(hipGetLastError());
+    int bad = 0;
+    MEV_HIP(hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost));
+    MEV_HIP(hipFree(d_bad));
+    if (bad) {  // not saturated at kmax: fall back to in-kernel evaluation
+      MEV_HIP(hipFree(c->util));
+      c->util = nullptr;
+      c->kp.util_direct = 1;
+    }
+  }
   MEV_HIP(hipDeviceSynchronize());
 
-  KParams& kp = c->kp;
-  kp.E = params->num_envs;
-  kp.U = params->num_ues;
-  kp.B = params->num_bs;
-  kp.W = params->width;
-  kp.H = params->height;
-  kp.t_end = params->ep_max_time < params->arrival_exit ? params->ep_max_time
-                                                         : params->arrival_exit;
-  kp.arr_start = params->arrival_start;
-  kp.arr_exit = params->arrival_exit;
-  kp.first_step_active = params->first_step_active;
-  kp.movement_reseed = params->movement_reseed;
-  kp.d2max = c->d2max;
-  kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
-  kp.Wd = (double)params->width;
-  kp.Hd = (double)params->height;
-  kp.vel = params->velocity;
-  kp.lower = params->util_lower;
-  kp.upper = params->util_upper;
-  kp.w1 = params->util_w1;
-  kp.w2 = params->util_w2;
-  kp.log_w3 = log(params->util_w3);
   *out = c;
   return MEV_OK;
 }
@@ -712,6 +819,7 @@ void mev_destroy(mev_ctx* c) {
   if (!c) return;
   (void)hipFree(c->rate_full);
   (void)hipFree(c->jump);
+  if (c->util) (void)hipFree(c->util);
   delete c;
 }
 
@@ -754,7 +862,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump};
+  KTables tb{c->rate_full, c->jump, c->util};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {

@@ -1,0 +1,97 @@
+"""GPU tests of the host surfaces: the MComCore/MComCustom facade (reference object API) and
+the batched make()/reset()/step() surface, against the reference fixtures and the oracle."""
+import random
+
+import numpy as np
+import pytest
+
+from helpers import load
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mcom_custom_facade_matches_reference():
+    from mobile_env.scenarios.custom import MComCustom
+    d = load("mcom_custom")
+    for k in range(8):
+        random.seed(int(d["random_seeds"][k]))
+        env = MComCustom()
+        users = [env.userDict[i] for i in sorted(env.userDict)]
+        s = 0
+        for ep in range(2):
+            env.reset()
+            lay = [[bs.point.x, bs.point.y] for bs in env.stationDict.values()]
+            assert lay == d["bs_xy"][k, ep, :d["bs_count"][k, ep]].tolist()
+            for _ in range(20):
+                env.step(ep, s % 20)
+                xy = [[ue.x, ue.y] for ue in users]
+                assert xy == d["xy"][k, s].tolist()
+                srv = [-1] * 7
+                for (bs, ue) in env.bs2ue_dataRates:
+                    srv[ue.ue_id] = bs.bs_id
+                assert srv == d["serving"][k, s].tolist()
+                rates = [float(env.allUserDataRates.get(ue, 0.0)) for ue in users]
+                assert rates == d["rate"][k, s].tolist()
+                ut = [env.ue_utilities.get(ue, np.nan) for ue in users]
+                np.testing.assert_allclose(ut, d["util"][k, s], rtol=1e-12)
+                sc = env.monitor.scalar_results
+                assert sc["number connections"][-1] == d["metrics"][k, s, 0]
+                np.testing.assert_allclose(sc["mean utility"][-1], d["metrics"][k, s, 2],
+                                           rtol=1e-5)
+                s += 1
+            assert env.time_is_up
+        env.close()
+
+
+def test_bare_core_first_step_is_noop():
+    """Bare MComCore.reset never refills activeUsers (reference base.py:75,172-209): the first
+    step of each episode moves nobody and reports mean utility = lower (metrics.py:26-27)."""
+    from mobile_env.core.base import MComCore
+    from mobile_env.core.entities import BaseStation, UserEquipment
+    cfg = MComCore.default_config()
+    st = [BaseStation(i, p, **cfg["bs"]) for i, p in enumerate([(50, 50), (150, 150)])]
+    us = [UserEquipment(i, **cfg["ue"]) for i in range(4)]
+    env = MComCore(st, us, {"seed": 5})
+    env.reset()
+    before = [(u.x, u.y) for u in us]
+    env.step(0, 0)
+    assert [(u.x, u.y) for u in us] == before
+    assert env.monitor.scalar_results["mean utility"][-1] == -20
+    assert len(env.activeUsers) == 4
+    env.step(0, 1)
+    assert env.monitor.scalar_results["number connected"][-1] >= 0
+    env.close()
+
+
+@pytest.mark.parametrize("env_id", ["mobile-small-central-v0", "mobile-medium-ma-v0",
+                                    "mobile-large-central-v0"])
+def test_make_reset_step_matches_oracle(env_id):
+    import mobile_env
+    from oracle.vec import OracleBatch, OracleParams
+    from mobile_env.scenarios.registry import LAYOUTS, spec
+    E = 64
+    env = mobile_env.make(env_id, num_envs=E, seed=300)
+    obs, info = env.reset()
+    sp = spec(env_id)
+    lay = LAYOUTS[sp["layout"]]
+    ob = OracleBatch(OracleParams(), lay["bs"], lay["num_ues"], np.arange(E) + 300)
+    ob.reset()
+    np.testing.assert_array_equal(env.engine.ue_xy.cpu().numpy(),
+                                  np.stack([ob.x, ob.y], -1))
+    for s in range(45):
+        obs, rew, term, trunc, info = env.step()
+        o = ob.step()
+        U = lay["num_ues"]
+        o4 = obs.cpu().numpy().reshape(E, U, 4)
+        np.testing.assert_array_equal(info["serving"].cpu().numpy(), o["serving"])
+        np.testing.assert_allclose(o4[..., 0], o["xy"][..., 0] / 200.0, rtol=1e-6)
+        np.testing.assert_allclose(o4[..., 2], o["rate"].astype(np.float32), rtol=1e-5)
+        if sp["mode"] == "central":
+            np.testing.assert_allclose(rew.cpu().numpy(), o["metrics"][:, 2], rtol=1e-5,
+                                       atol=1e-7)
+        else:
+            np.testing.assert_allclose(rew.cpu().numpy(), o["util"].astype(np.float32),
+                                       rtol=1e-5, atol=1e-7)
+        np.testing.assert_array_equal(trunc.cpu().numpy(), o["done"])
+        assert not term.any()
+    env.close()

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU session script (dev): tests, smoke, bench, rocprof kernel trace
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/smoke.log; exit 1; }
+cat gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; cat gpurun_out/bench.log; exit 1; }
+cat gpurun_out/bench.log
+cd /tmp && export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python3 bench.py --profile-run --steps 200 --warmup 20 > gpurun_out/prof_kt.log 2>&1 || { echo prof failed; tail -20 gpurun_out/prof_kt.log; exit 1; }
+find gpurun_out/prof_kt -name "*stats*" | head
