@@ -20,8 +20,9 @@
  *     `stream` (NULL = default stream). A context is not thread-safe; use one
  *     context per (device, stream).
  *   - Layout (SoA, row-major, E envs, U UEs, B base stations per env):
- *       ue_xy   int32 [E][U][2]   UE position (integer grid, entities.py:52-54)
- *       wp_xy   int32 [E][U][2]   RandomWaypoint target; x < 0 means "no waypoint"
+ *       ue_state int32 [E][U][4]  {x, y, wx, wy}: UE position (integer grid,
+ *                                 entities.py:52-54) and RandomWaypoint target
+ *                                 (movement.py:44-47); wx < 0 means "no waypoint"
  *       pcg     uint64[E][6]      numpy-PCG64 stream of the movement model:
  *                                 {state_lo, state_hi, inc_lo, inc_hi,
  *                                  state0_lo, state0_hi}; state0 = state right after
@@ -82,8 +83,7 @@ typedef struct mev_params {
 } mev_params;
 
 typedef struct mev_state {
-  int32_t* ue_xy;
-  int32_t* wp_xy;
+  int32_t* ue_state;
   uint64_t* pcg;
   int32_t* t;
   const int32_t* bs_xy;

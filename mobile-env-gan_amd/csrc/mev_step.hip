@@ -37,6 +37,7 @@
 #include "mev.h"
 
 typedef unsigned __int128 u128;
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 // numpy PCG64 = PCG XSL-RR 128/64 (numpy/random/src/pcg64/pcg64.h)
 #define PCG_MULT_HI 0x2360ED051FC65DA4ULL
@@ -46,7 +47,8 @@ namespace {
 
 constexpr int kMaxU = 1024;
 constexpr int kMaxB = 1024;
-constexpr int kKeyBits = 10;  // BS index bits in the packed (d2, bs) association key
+constexpr int kKeyBits = 10;
+constexpr int kMaxSharedBS = 1024;  // shared-layout stations staged in LDS (8 KB)  // BS index bits in the packed (d2, bs) association key
 
 struct KParams {
   int E, U, B, W, H;
@@ -59,12 +61,15 @@ struct KParams {
   int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
   int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
   float inv_w, inv_h; // obs normalisation
+  int d2snap;         // largest integer d2 with sqrt(d2) <= velocity (arrival test)
+  float move_band;    // tie band of the float32 movement fast path
+  int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
+  float vel_f;
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
 };
 
 struct KState {
-  int2* ue_xy;
-  int2* wp_xy;
+  int4* ue_state;  // [E][U] {x, y, wx, wy}
   uint64_t* pcg;
   int* t;
   const int2* bs_xy;
@@ -85,6 +90,7 @@ struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
   const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
+  const double* c100;       // [U + 1]: 100.0 / n  (fast path of the share rounding)
 };
 
 // ------------------------------------------------------------------------------------
@@ -175,17 +181,51 @@ __device__ double pairwise_any(const double* a, int n) {
   return ret;
 }
 
-// Per-UE movement (movement.py:42-62). Waypoint already drawn if needed.
-__device__ __forceinline__ void move_ue(int2& pos, int2& wp, double vel) {
+// Per-UE movement (movement.py:42-62), exact float64 form: the reference computes
+// position + velocity * v / |v| in float64, then np.round (half-to-even) and astype(int).
+__device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel) {
+  const double nrm = sqrt((double)(dx * dx + dy * dy));  // np.linalg.norm of the int vector
+  return make_int2((int)rint((double)pos.x + (vel * (double)dx) / nrm),
+                   (int)rint((double)pos.y + (vel * (double)dy) / nrm));
+}
+
+// true when q is farther than `band` from the nearest half-integer
+__device__ __forceinline__ bool clear_of_tie(float q, float band) {
+  const float f = q - floorf(q);  // exact
+  return fabsf(f - 0.5f) > band;
+}
+
+// Movement step. Arrival (|v| <= velocity) is the integer test d2 <= d2snap (sqrt is
+// correctly rounded and monotone). Otherwise the new coordinate is x + rint(q) with
+// q = velocity * dx / |v| (x is an integer, so rint(x + q) = x + rint(q) unless x + q is a
+// tie). q is evaluated in float32 with a relative error < 5e-7 (|q| <= velocity, so the
+// absolute error is < 5e-7 * max(1, velocity)); only when q lies within move_band =
+// 2^-16 * max(1, velocity) (30x wider) of a half-integer -- where float32 could pick the
+// other integer, or half-to-even needs the exact value -- is the exact float64 form used. Axis-parallel
+// moves (q = +-velocity exactly) are done exactly in float64 (no division needed).
+__device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
   const int dx = wp.x - pos.x;
   const int dy = wp.y - pos.y;
-  const double nrm = sqrt((double)(dx * dx + dy * dy));  // np.linalg.norm of int vector
-  if (nrm <= vel) {  // arrived: snap to waypoint and pop it
+  const int d2 = dx * dx + dy * dy;
+  if (d2 <= kp.d2snap) {  // arrived: snap to waypoint and pop it
     pos = wp;
     wp = make_int2(-1, -1);
-  } else {  // position + velocity * v / |v|, np.round (half-to-even), astype(int)
-    pos.x = (int)rint((double)pos.x + (vel * (double)dx) / nrm);
-    pos.y = (int)rint((double)pos.y + (vel * (double)dy) / nrm);
+    return;
+  }
+  if (kp.axis_exact && (dx == 0 || dy == 0)) {
+    const double q = kp.vel;
+    if (dy == 0) pos.x = (int)rint((double)pos.x + (dx > 0 ? q : -q));
+    else pos.y = (int)rint((double)pos.y + (dy > 0 ? q : -q));
+    return;
+  }
+  const float r = __builtin_amdgcn_rsqf((float)d2);
+  const float qx = kp.vel_f * (float)dx * r;
+  const float qy = kp.vel_f * (float)dy * r;
+  if (clear_of_tie(qx, kp.move_band) && clear_of_tie(qy, kp.move_band)) {
+    pos.x += (int)rintf(qx);
+    pos.y += (int)rintf(qy);
+  } else {
+    pos = move_exact(pos, dx, dy, kp.vel);
   }
 }
 
@@ -201,12 +241,16 @@ __device__ __forceinline__ double scaled_utility(double rate, const KParams& kp)
   return 2.0 * (ur - kp.lower) / (kp.upper - kp.lower) - 1.0;
 }
 
-// ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435):
-// rint(share * 100) / 100. Returns the rate; `cents` gets rint(share * 100).
-__device__ __forceinline__ double shared_rate(double full, int n, double& cents) {
-  const double share = full / (double)n;
-  cents = rint(share * 100.0);
-  return cents / 100.0;
+// ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435): the
+// reference value is cents = rint(fl(fl(full / n) * 100)), rate = cents / 100. The fast path
+// forms c = full * fl(100 / n) (within 2^-51 relative of the exact product) and rounds it
+// directly; only when c lies within 2^-46 relative of a half-integer are the two exact
+// float64 operations evaluated. Returns cents (an integer-valued double).
+__device__ __forceinline__ double share_cents(double full, int n, const double* __restrict__ c100) {
+  const double c = full * c100[n];
+  const double f = c - floor(c);
+  if (fabs(f - 0.5) > c * 0x1p-46) return rint(c);
+  return rint((full / (double)n) * 100.0);
 }
 
 // Scaled utility of a rounded rate. The utility depends on the rate only, and the rate is
@@ -220,161 +264,192 @@ __device__ __forceinline__ double utility_of(double rate, double cents, const KP
   return kp.util_sat;
 }
 
-// ------------------------------------------------------------------------------------
-// Packed kernel: U <= 64, floor(64/U) envs per wavefront, one lane per UE.
-// RESET=true: only re-initialise envs (optionally masked), write reset obs.
-// ------------------------------------------------------------------------------------
 constexpr int kPackedBlock = 256;
 constexpr int kWavesPerBlock = kPackedBlock / 64;
 
-__device__ __forceinline__ void wave_lds_sync() {
-  // LDS written by other lanes of this wavefront becomes visible (no workgroup barrier)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
-// numpy pairwise sum (n <= 64) of the values `v` of the lanes selected by `mtake` inside one
-// env segment (lanes base..base+U-1), in lane order. The 8 block accumulators live in
-// lanes base..base+7 and are combined by a butterfly that reproduces numpy's
-// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)). Result valid in lane `base`. Called by all lanes.
-__device__ __forceinline__ double seg_pairwise_sum(double v, bool take, uint64_t mtake,
-                                                   uint64_t lt, int base, int u,
-                                                   double* __restrict__ lds) {
-  const int n = __popcll(mtake);
-  if (take) lds[base + __popcll(mtake & lt)] = v;
-  wave_lds_sync();
-  const int nfull = n - (n & 7);
-  double r = 0.0;
-  if (n >= 8 && u < 8) {
-    r = lds[base + u];
-    for (int i = 8; i < nfull; i += 8) r += lds[base + i + u];
+// Sum of `v` over the lanes of one env segment that have `take` set (segment = lanes
+// base..base+U-1, u = lane - base): a shift-down tree in float64 with partners restricted to
+// the segment; the result is valid in lane `base`. (numpy's np.mean sums in pairwise order;
+// the two float64 sums differ by a few ulps at most, far below the float32 output.)
+__device__ __forceinline__ double seg_sum(double v, bool take, int U, int u) {
+  double x = take ? v : 0.0;
+  for (int off = 1; off < U; off <<= 1) {
+    const double y = __shfl_down(x, (unsigned)off);
+    if (u + off < U) x += y;
   }
-  r += __shfl(r, base + (u ^ 1));
-  r += __shfl(r, base + (u ^ 2));
-  r += __shfl(r, base + (u ^ 4));
-  double res = r;
-  if (u == 0) {
-    int i = nfull;
-    if (n < 8) {
-      res = -0.0;
-      i = 0;
-    }
-    for (; i < n; ++i) res += lds[base + i];
-  }
-  return res;
+  return x;
 }
 
 // ------------------------------------------------------------------------------------
-// Packed kernel: U <= 64, floor(64/U) envs per wavefront, one lane per UE.
-// RESET=true: only re-initialise envs (optionally masked), write reset obs.
+// Packed shape: U <= 64, G = floor(64/U) envs per wavefront, one lane per UE.
 // ------------------------------------------------------------------------------------
-template <bool PER_ENV_BS, bool RESET>
-__global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
-                                                             KTables tb,
-                                                             const uint8_t* __restrict__ mask) {
-  __shared__ double lds_util[kWavesPerBlock][64];
-  __shared__ double lds_rate[kWavesPerBlock][64];
+struct LaneMap {
+  int seg, u, base;
+  uint64_t segmask, lt;
+};
 
+__device__ __forceinline__ LaneMap lane_map(int lane, int U) {
+  LaneMap m;
+  // lane / U through float: (lane + 0.5) / U is >= 0.5/U away from an integer
+  m.seg = (int)(((float)lane + 0.5f) * (1.0f / (float)U));
+  m.u = lane - m.seg * U;
+  m.base = m.seg * U;
+  m.segmask = (U >= 64) ? ~0ull : (((1ull << U) - 1ull) << m.base);
+  m.lt = (1ull << lane) - 1ull;
+  return m;
+}
+
+// Per-lane inputs of one env group that are prefetched one group ahead of use. The loads
+// are unconditional (index clamped to a valid env): a guarded load would make the compiler
+// wait for it at the merge point, which defeats the prefetch.
+struct GroupIn {
+  int t;
+  int4 s;  // {x, y, wx, wy}
+};
+
+__device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st, int e, int u) {
+  const int ec = min(e, kp.E - 1);
+  GroupIn g;
+  g.t = st.t[ec];
+  g.s = st.ue_state[(size_t)ec * kp.U + u];
+  return g;
+}
+
+// Reset kernel: MComCore.reset (base.py:172-209) for envs with mask[e] != 0 (all if NULL):
+// movement RNG re-seeded (movement.py:16-18), initial positions in ue_id order, 2 draws per
+// UE (movement.py:64-72), waypoints cleared, t = 0.
+__global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KState st, KOut out,
+                                                              KTables tb,
+                                                              const uint8_t* __restrict__ mask) {
   const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
-  const int wave = blockIdx.x * kWavesPerBlock + wib;
-  const int U = kp.U;
-  const int G = kp.envs_per_wave;
-  const int seg = lane / U;
-  const int u = lane - seg * U;
-  const int base = seg * U;
-  const int e = wave * G + seg;
-  const bool valid = (seg < G) && (e < kp.E);
-  const uint64_t segmask = (U >= 64) ? ~0ull : (((1ull << U) - 1ull) << base);
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const size_t idx = (size_t)e * U + u;
-
-  // all loads first (no load waits on another): env row, then this UE's state
-  int t = 0;
-  int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
-  ulonglong2 pa = make_ulonglong2(0, 0), pb = pa, pc = pa;
-  bool msk = true;
-  if (valid) {
-    const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e);
-    pa = pr[0];
-    pb = pr[1];
-    pc = pr[2];
-    if (RESET) {
-      msk = (mask == nullptr) || mask[e];
-    } else {
-      t = st.t[e];
-      pos = st.ue_xy[idx];
-      wp = st.wp_xy[idx];
-    }
+  const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const LaneMap m = lane_map(lane, kp.U);
+  const int e = wave * kp.envs_per_wave + m.seg;
+  if (m.seg >= kp.envs_per_wave || e >= kp.E) return;
+  if (mask != nullptr && !mask[e]) return;
+  const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e);
+  const ulonglong2 pa = pr[0], pb = pr[1], pc = pr[2];
+  const u128 inc = mk128(pb.x, pb.y);
+  const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : mk128(pa.x, pa.y);
+  u128 su = pcg_advance(s0, inc, 2 * m.u, tb.jump);
+  const int x = pcg_draw_coord(su, inc, kp.Wd);
+  const int y = pcg_draw_coord(su, inc, kp.Hd);
+  const size_t idx = (size_t)e * kp.U + m.u;
+  st.ue_state[idx] = make_int4(x, y, -1, -1);
+  out.serving[idx] = -1;
+  out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
+  if (out.rate64) out.rate64[idx] = 0.0;
+  if (out.util64) out.util64[idx] = 0.0;
+  if (m.u == 0) {
+    const u128 s = pcg_advance(s0, inc, 2 * kp.U, tb.jump);
+    *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+        make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+    st.t[e] = 0;
+    out.reward[e] = 0.f;
+    out.done[e] = 0;
+    if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+}
+
+// One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
+template <bool PER_ENV_BS>
+__device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
+                                                const KOut& out, const KTables& tb,
+                                                const LaneMap& m, const GroupIn& cur, int e,
+                                                bool valid,
+                                                const int2* __restrict__ lds_bsm) {
+  const int U = kp.U;
+  const int u = m.u;
+  const uint64_t segmask = m.segmask, lt = m.lt;
+  const bool want_metrics = out.metrics != nullptr;
+  const bool want_rate = out.rate64 != nullptr || want_metrics || kp.util_direct;
+  // PCG64 row of this env: consumed only by waypoint draws, resets and the state update,
+  // so it is loaded here and its latency hides under the association work
+  const ulonglong2* pr =
+      reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * min(e, kp.E - 1));
+  const ulonglong2 pa = pr[0], pb = pr[1];
+
+  const size_t idx = (size_t)e * U + u;
+  int t = cur.t;
+  int2 pos = make_int2(cur.s.x, cur.s.y);
+  int2 wp = make_int2(cur.s.z, cur.s.w);
   const u128 inc = mk128(pb.x, pb.y);
   u128 s = mk128(pa.x, pa.y);
-  const bool do_reset = valid && (RESET ? msk : (t >= kp.t_end));
-  if (do_reset) {
-    // MComCore.reset (base.py:172-209): movement RNG re-seeded (movement.py:16-18),
-    // initial positions in ue_id order, 2 draws per UE (movement.py:64-72).
-    const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : s;
-    u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
-    pos.x = pcg_draw_coord(su, inc, kp.Wd);
-    pos.y = pcg_draw_coord(su, inc, kp.Hd);
-    s = pcg_advance(s0, inc, 2 * U, tb.jump);
-    wp = make_int2(-1, -1);
-    t = 0;
-  }
 
-  if (RESET) {
-    if (do_reset) {
-      st.ue_xy[idx] = pos;
-      st.wp_xy[idx] = wp;
-      out.serving[idx] = -1;
-      out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
-      if (out.rate64) out.rate64[idx] = 0.0;
-      if (out.util64) out.util64[idx] = 0.0;
-      if (u == 0) {
-        uint64_t* pw = st.pcg + (size_t)6 * e;
-        *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
-        st.t[e] = 0;
-        out.reward[e] = 0.f;
-        out.done[e] = 0;
-        if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+  // ---- lazy auto-reset at the start of the step after the episode ended ---------------
+  const bool do_reset = valid && t >= kp.t_end;
+  if (__ballot(do_reset)) {
+    if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
+      const ulonglong2 pc =
+          reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
+      const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : s;
+      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
+      pos.x = pcg_draw_coord(su, inc, kp.Wd);
+      pos.y = pcg_draw_coord(su, inc, kp.Hd);
+      s = pcg_advance(s0, inc, 2 * U, tb.jump);
+      wp = make_int2(-1, -1);
+      t = 0;
     }
-    return;
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
   const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
                       (kp.first_step_active || t != 0);
 
-  // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ----------
+  // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ------------
   const bool need = active && wp.x < 0;
-  const uint64_t mneed = __ballot(need) & segmask;
-  if (need) {
-    u128 su = pcg_advance(s, inc, 2 * __popcll(mneed & lt), tb.jump);
-    wp.x = pcg_draw_coord(su, inc, kp.Wd);
-    wp.y = pcg_draw_coord(su, inc, kp.Hd);
-  }
-  if (active) move_ue(pos, wp, kp.vel);
-
-  // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
-  unsigned best = UINT_MAX;
-  if (active) {
-    const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
-    const int2* bs = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
-    for (int b = 0; b < nb; ++b) {
-      const int2 p = bs[b];
-      const int ddx = pos.x - p.x;
-      const int ddy = pos.y - p.y;
-      const unsigned key = ((unsigned)(ddx * ddx + ddy * ddy) << kKeyBits) | (unsigned)b;
-      best = min(best, key);  // ties -> lowest bs index, like python min() over stations
+  const uint64_t mneed_w = __ballot(need);
+  const uint64_t mneed = mneed_w & segmask;
+  if (mneed_w) {
+    if (need) {
+      u128 su = pcg_advance(s, inc, 2 * __popcll(mneed & lt), tb.jump);
+      wp.x = pcg_draw_coord(su, inc, kp.Wd);
+      wp.y = pcg_draw_coord(su, inc, kp.Hd);
     }
   }
-  const int d2s = (int)(best >> kKeyBits);
-  const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+  if (active) move_ue(pos, wp, kp);
 
-  // ---- 3. n_b for the own serving BS: lanes of the segment with the same index, found by
-  //         matching the index bit by bit with ballots (no LDS, no atomics) ---------------
+  // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
+  // key = (e << 10) | j, min over stations j: ties keep the lower index (python min() over
+  // the station dict). Shared layout: e = d2 - |p|^2 + 2^21 = |q|^2 + 2^21 - 2 p.q is ONE
+  // packed-int16 dot product per station with the per-station constants from LDS (|p|^2 is
+  // the same for every station, so the argmin is unchanged). Per-env layout: e = d2.
+  unsigned best = UINT_MAX;
+  const s16x2 pu = {(short)pos.x, (short)pos.y};
+  if (PER_ENV_BS) {
+    const int nb = st.bs_count ? (valid ? st.bs_count[e] : 0) : kp.B;
+    const int2* bs = st.bs_xy + (size_t)e * kp.B;
+    if (active && nb > 0) {
+      const int nb8 = (kp.B + 7) & ~7;  // wave-uniform trip count; j clamped to the last
+      for (int b0 = 0; b0 < nb8; b0 += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int j = min(b0 + k, nb - 1);
+          const int2 p = bs[j];
+          const s16x2 d = pu - s16x2{(short)p.x, (short)p.y};  // coordinates < 1024
+          const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
+          best = min(best, (d2 << kKeyBits) | (unsigned)j);
+        }
+      }
+    }
+  } else if (active) {
+    const int nb = kp.B;
+#pragma unroll 4
+    for (int j = 0; j < nb; ++j) {
+      const int2 mc = lds_bsm[j];  // {(-2qx, -2qy) as int16x2, |q|^2 + 2^21}
+      const unsigned ev = (unsigned)__builtin_amdgcn_sdot2(
+          pu, __builtin_bit_cast(s16x2, mc.x), mc.y, false);
+      best = min(best, (ev << kKeyBits) | (unsigned)j);
+    }
+  }
+  const int d2s = PER_ENV_BS ? (int)(best >> kKeyBits)
+                             : (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
+  const int srv =
+      (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+
+  // ---- 3. n_b of the own serving BS: lanes of the segment with the same index, matched
+  //         bit by bit with ballots (no LDS, no atomics) ---------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
   uint64_t match = mcon;
   for (int bit = 0; bit < kp.srv_bits; ++bit) {
@@ -384,34 +459,35 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   }
   const int n = __popcll(match);
 
-  // ---- 4. rate + utility -------------------------------------------------------------
-  double rate = 0.0, cents = 0.0;
-  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], n, cents);
+  // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
+  double cents = 0.0, rate = 0.0;
+  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], n, tb.c100);
+  if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
 
-  // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) -----
+  // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
   const uint64_t mact = __ballot(active) & segmask;
   const int nact = __popcll(mact);
-  const double sum_u = seg_pairwise_sum(util, active, mact, lt, base, u, lds_util[wib]);
-  const bool want_metrics = out.metrics != nullptr;
+  const double sum_u = seg_sum(util, active, U, u);
   double sum_r = 0.0;
-  if (want_metrics) sum_r = seg_pairwise_sum(rate, srv >= 0, mcon, lt, base, u, lds_rate[wib]);
+  if (want_metrics) sum_r = seg_sum(rate, srv >= 0, U, u);
 
-  // ---- 6. stores ---------------------------------------------------------------------
+  // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
-    st.ue_xy[idx] = pos;
-    st.wp_xy[idx] = wp;
+    st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
     out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, (float)rate,
-                               (float)util);
+    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
+                               (float)cents * 0.01f, (float)util);
     if (out.rate64) out.rate64[idx] = rate;
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
     if (u == 0) {
       const double mean_u = nact > 0 ? sum_u / (double)nact : kp.lower;
-      const u128 s_next = pcg_advance(s, inc, 2 * __popcll(mneed), tb.jump);
-      uint64_t* pw = st.pcg + (size_t)6 * e;
-      *reinterpret_cast<ulonglong2*>(pw) =
-          make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
+      const int tot = __popcll(mneed);
+      if (tot || t == 0) {  // the stream moved (draws, or reset): write the new state back
+        const u128 s_next = tot ? pcg_advance(s, inc, 2 * tot, tb.jump) : s;
+        *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+            make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
+      }
       st.t[e] = t + 1;
       out.reward[e] = (float)mean_u;
       out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
@@ -422,6 +498,31 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
       }
     }
   }
+
+}
+
+// Step kernel: one env group per wavefront (latency hidden by occupancy: 8 waves/SIMD).
+template <bool PER_ENV_BS>
+__global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
+                                                              KTables tb, int ngroups) {
+  __shared__ int2 lds_bsm[PER_ENV_BS ? 1 : kMaxSharedBS];
+  if (!PER_ENV_BS) {  // per-station constants of the association dot product
+    for (int i = threadIdx.x; i < kp.B; i += blockDim.x) {
+      const int2 q = st.bs_xy[i];
+      const s16x2 m2 = {(short)(-2 * q.x), (short)(-2 * q.y)};
+      lds_bsm[i] = make_int2(__builtin_bit_cast(int, m2), q.x * q.x + q.y * q.y + (1 << 21));
+    }
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const int g = blockIdx.x * kWavesPerBlock + wib;
+  if (g >= ngroups) return;
+  const LaneMap m = lane_map(lane, kp.U);
+  const int e = g * kp.envs_per_wave + m.seg;
+  const bool valid = (m.seg < kp.envs_per_wave) && (e < kp.E);
+  const GroupIn a = load_group(kp, st, e, m.u);
+  packed_group<PER_ENV_BS>(kp, st, out, tb, m, a, e, valid, lds_bsm);
 }
 
 // ------------------------------------------------------------------------------------
@@ -468,15 +569,15 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   } else {
     s = mk128(a.x, a.y);
     if (valid) {
-      pos = st.ue_xy[idx];
-      wp = st.wp_xy[idx];
+      const int4 sv = st.ue_state[idx];
+      pos = make_int2(sv.x, sv.y);
+      wp = make_int2(sv.z, sv.w);
     }
   }
 
   if (RESET) {
     if (valid) {
-      st.ue_xy[idx] = pos;
-      st.wp_xy[idx] = wp;
+      st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
       out.serving[idx] = -1;
       out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
       if (out.rate64) out.rate64[idx] = 0.0;
@@ -519,18 +620,19 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     wp.x = pcg_draw_coord(su, inc, kp.Wd);
     wp.y = pcg_draw_coord(su, inc, kp.Hd);
   }
-  if (active) move_ue(pos, wp, kp.vel);
+  if (active) move_ue(pos, wp, kp);
 
   // ---- 2. association (BS coordinates are workgroup-uniform: scalar loads) ------------
   unsigned best = UINT_MAX;
   if (active) {
     const int2* bs = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+    const s16x2 pu = {(short)pos.x, (short)pos.y};
 #pragma unroll 8
     for (int b = 0; b < nb; ++b) {
       const int2 p = bs[b];
-      const int ddx = pos.x - p.x;
-      const int ddy = pos.y - p.y;
-      const unsigned key = ((unsigned)(ddx * ddx + ddy * ddy) << kKeyBits) | (unsigned)b;
+      const s16x2 d = pu - s16x2{(short)p.x, (short)p.y};
+      const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
+      const unsigned key = (d2 << kKeyBits) | (unsigned)b;
       best = min(best, key);
     }
   }
@@ -550,8 +652,9 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   }
 
   // ---- 4. rate + utility -------------------------------------------------------------
-  double rate = 0.0, cents = 0.0;
-  if (srv >= 0) rate = shared_rate(tb.rate_full[d2s], lds_cnt[srv], cents);
+  double cents = 0.0, rate = 0.0;
+  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv], tb.c100);
+  if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
   if (active) lds_util[pre_act + __popcll(mact & lt)] = util;
   const bool want_metrics = out.metrics != nullptr;
@@ -559,11 +662,10 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   __syncthreads();
 
   if (valid) {
-    st.ue_xy[idx] = pos;
-    st.wp_xy[idx] = wp;
+    st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
     out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, (float)rate,
-                               (float)util);
+    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
+                               (float)cents * 0.01f, (float)util);
     if (out.rate64) out.rate64[idx] = rate;
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
   }
@@ -656,6 +758,7 @@ struct mev_ctx {
   double* rate_full;
   u128* jump;
   double* util;
+  double* c100;
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -734,6 +837,19 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.srv_bits = 0;
   while ((1 << kp.srv_bits) < params->num_bs) ++kp.srv_bits;
   kp.util_sat = 2.0 * (kp.upper - kp.lower) / (kp.upper - kp.lower) - 1.0;
+  kp.vel_f = (float)params->velocity;
+  kp.move_band = 0x1p-16f * (params->velocity > 1.0 ? (float)params->velocity : 1.0f);
+  {  // arrival threshold and axis-parallel exactness (host IEEE float64 == device)
+    const int d2_top = (params->width - 1) * (params->width - 1) +
+                       (params->height - 1) * (params->height - 1);
+    int d2 = 0;
+    while (d2 <= d2_top && sqrt((double)d2) <= params->velocity) ++d2;
+    kp.d2snap = d2 - 1;
+    kp.axis_exact = 1;
+    const int amax = params->width > params->height ? params->width : params->height;
+    for (int a = 1; a <= amax; ++a)
+      if ((params->velocity * (double)a) / (double)a != params->velocity) kp.axis_exact = 0;
+  }
   // utility saturation point r_sat = w3^(upper/w1) - w2 (increasing utility only)
   kp.util_direct = 1;
   kp.util_kmax = 0;
@@ -784,6 +900,25 @@ int mev_create(const mev_params* params, mev_ctx** out) {
                      c->jump);
   MEV_HIP(hipGetLastError());
 
+  // ---- 100 / n for the share rounding fast path ----
+  {
+    const int nmax = params->num_ues;
+    double* h = (double*)malloc(sizeof(double) * (size_t)(nmax + 1));
+    if (!h || hipMalloc(&c->c100, sizeof(double) * (size_t)(nmax + 1)) != hipSuccess) {
+      free(h);
+      (void)hipFree(c->rate_full);
+      (void)hipFree(c->jump);
+      delete c;
+      return MEV_ENOMEM;
+    }
+    h[0] = 0.0;
+    for (int n = 1; n <= nmax; ++n) h[n] = 100.0 / (double)n;
+    const hipError_t e = hipMemcpy(c->c100, h, sizeof(double) * (size_t)(nmax + 1),
+                                   hipMemcpyHostToDevice);
+    free(h);
+    MEV_HIP(e);
+  }
+
   // ---- utility table over rounded rates ----
   c->util = nullptr;
   if (!c->kp.util_direct) {
@@ -820,6 +955,7 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->rate_full);
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
+  (void)hipFree(c->c100);
   delete c;
 }
 
@@ -835,14 +971,13 @@ int mev_copy_rate_table(const mev_ctx* c, double* dst, int64_t n) {
 
 static int check_bufs(const mev_ctx* c, const mev_state* st, const mev_outputs* out) {
   if (!c || !st || !out) return MEV_EINVAL;
-  if (!st->ue_xy || !st->wp_xy || !st->pcg || !st->t || !st->bs_xy) return MEV_EINVAL;
+  if (!st->ue_state || !st->pcg || !st->t || !st->bs_xy) return MEV_EINVAL;
   if (!out->obs || !out->serving || !out->reward || !out->done) return MEV_EINVAL;
   return MEV_OK;
 }
 
 static void to_kernel(const mev_state* st, const mev_outputs* out, KState& ks, KOut& ko) {
-  ks.ue_xy = reinterpret_cast<int2*>(st->ue_xy);
-  ks.wp_xy = reinterpret_cast<int2*>(st->wp_xy);
+  ks.ue_state = reinterpret_cast<int4*>(st->ue_state);
   ks.pcg = st->pcg;
   ks.t = st->t;
   ks.bs_xy = reinterpret_cast<const int2*>(st->bs_xy);
@@ -862,18 +997,25 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util};
+  KTables tb{c->rate_full, c->jump, c->util, c->c100};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
-    const long waves = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
-    const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
-    if (per_env)
-      hipLaunchKernelGGL((k_step_packed<true, RESET>), grid, dim3(kPackedBlock), 0, stream, kp,
-                         ks, ko, tb, mask);
-    else
-      hipLaunchKernelGGL((k_step_packed<false, RESET>), grid, dim3(kPackedBlock), 0, stream, kp,
-                         ks, ko, tb, mask);
+    const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
+    if (RESET) {
+      const dim3 grid((unsigned)((groups + kWavesPerBlock - 1) / kWavesPerBlock));
+      hipLaunchKernelGGL(k_reset_packed, grid, dim3(kPackedBlock), 0, stream, kp, ks, ko, tb,
+                         mask);
+    } else {
+      // persistent: at most c->resident_blocks workgroups, each wave walks several groups
+      const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+      if (per_env)
+        hipLaunchKernelGGL((k_step_packed<true>), dim3(blocks), dim3(kPackedBlock), 0, stream,
+                           kp, ks, ko, tb, groups);
+      else
+        hipLaunchKernelGGL((k_step_packed<false>), dim3(blocks), dim3(kPackedBlock), 0, stream,
+                           kp, ks, ko, tb, groups);
+    }
   } else {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
     if (per_env)

@@ -43,8 +43,8 @@ class MevParams(C.Structure):
 
 
 class MevState(C.Structure):
-    _fields_ = [("ue_xy", C.c_void_p), ("wp_xy", C.c_void_p), ("pcg", C.c_void_p),
-                ("t", C.c_void_p), ("bs_xy", C.c_void_p), ("bs_count", C.c_void_p)]
+    _fields_ = [("ue_state", C.c_void_p), ("pcg", C.c_void_p), ("t", C.c_void_p),
+                ("bs_xy", C.c_void_p), ("bs_count", C.c_void_p)]
 
 
 class MevOutputs(C.Structure):

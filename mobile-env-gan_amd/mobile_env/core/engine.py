@@ -8,9 +8,10 @@ reference keeps in entity/plugin objects:
 =====================  ===================================  ============================
 tensor                 reference state                      reference file:line
 =====================  ===================================  ============================
-``ue_xy [E,U,2] i32``  ``UserEquipment.x/.y``               entities.py:47-48, base.py:233
-``wp_xy [E,U,2] i32``  ``RandomWaypointMovement``           movement.py:33,44-47,55
-                       ``.userMoveDirection`` (x<0: none)
+``ue_state [E,U,4]``   ``UserEquipment.x/.y`` (cols 0-1)    entities.py:47-48, base.py:233
+  ``i32``              ``RandomWaypointMovement``           movement.py:33,44-47,55
+                       ``.userMoveDirection`` (cols 2-3,
+                       wx<0: none)
 ``pcg [E,6] u64``      ``Movement.rng`` (numpy PCG64)       movement.py:16-18
 ``t [E] i32``          ``MComCore.time``                    base.py:175,280
 ``bs_xy [B,2]/[E,B,2]`` ``BaseStation.x/.y`` (int-truncated) entities.py:18,24-26
@@ -113,8 +114,7 @@ class StepEngine:
                 self.bs_count = torch.as_tensor(bs_count, dtype=torch.int32).reshape(E).to(**kw)
                 if int(self.bs_count.max()) > B or int(self.bs_count.min()) < 0:
                     raise ValueError("bs_count out of range")
-            self.ue_xy = torch.zeros((E, U, 2), dtype=torch.int32, **kw)
-            self.wp_xy = torch.full((E, U, 2), -1, dtype=torch.int32, **kw)
+            self.ue_state = torch.full((E, U, 4), -1, dtype=torch.int32, **kw)
             self.t = torch.full((E,), params.t_end, dtype=torch.int32, **kw)
             self.pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
             self.obs = torch.zeros((E, U, 4), dtype=torch.float32, **kw)
@@ -129,7 +129,7 @@ class StepEngine:
 
     # -- plumbing -----------------------------------------------------------------------------
     def _bind(self):
-        self._st = N.MevState(_ptr(self.ue_xy), _ptr(self.wp_xy), _ptr(self.pcg), _ptr(self.t),
+        self._st = N.MevState(_ptr(self.ue_state), _ptr(self.pcg), _ptr(self.t),
                               _ptr(self.bs_xy), _ptr(self.bs_count))
         self._out = N.MevOutputs(_ptr(self.obs), _ptr(self.serving), _ptr(self.reward),
                                  _ptr(self.done), _ptr(self.rate64), _ptr(self.util64),
@@ -137,6 +137,16 @@ class StepEngine:
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def ue_xy(self):
+        """UE positions [E,U,2] (view of ue_state)."""
+        return self.ue_state[..., :2]
+
+    @property
+    def wp_xy(self):
+        """RandomWaypoint targets [E,U,2] (view of ue_state; x < 0: none)."""
+        return self.ue_state[..., 2:]
 
     @property
     def d2max(self) -> int:

@@ -10,5 +10,5 @@ timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench fa
 cat gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python3 bench.py --profile-run --steps 200 --warmup 20 > gpurun_out/prof_kt.log 2>&1 || { echo prof failed; tail -20 gpurun_out/prof_kt.log; exit 1; }
-find gpurun_out/prof_kt -name "*stats*" | head
+tools/profile.sh ${PROFILE_TAG:-dev} || exit 1
+

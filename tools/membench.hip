@@ -1,0 +1,58 @@
+// Dev tool: memory floor of the step kernel's access pattern on MI355X (no compute).
+//  kind 0: same lane mapping / loads / stores as the packed step kernel, trivial math
+//  kind 1: ideal streaming with the same read:write byte ratio (float4 read, 2x float4 write)
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+__global__ __launch_bounds__(256) void k_pattern(int4* st, uint64_t* pcg, int* t, float4* obs,
+                                                int* serving, float* reward, uint8_t* done,
+                                                int E, int U) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int G = 64 / U;
+  const int seg = lane / U;
+  const int u = lane - seg * U;
+  const int e = wave * G + seg;
+  if (seg >= G || e >= E) return;
+  const size_t idx = (size_t)e * U + u;
+  const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(pcg + 6 * (size_t)e);
+  const ulonglong2 a = pr[0], b = pr[1];
+  const int tt = t[e];
+  int4 s = st[idx];
+  s.x += 1;
+  s.y += (int)(a.x & 1);
+  st[idx] = s;
+  serving[idx] = s.z;
+  obs[idx] = make_float4((float)s.x, (float)s.y, (float)tt, (float)(b.y & 7));
+  if (u == 0) {
+    *reinterpret_cast<ulonglong2*>(pcg + 6 * (size_t)e) = make_ulonglong2(a.x + 1, a.y);
+    t[e] = tt + 1;
+    reward[e] = (float)tt;
+    done[e] = (uint8_t)(tt > 19);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stream(const float4* __restrict__ in, float4* __restrict__ out,
+                                               size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 v = in[i];
+  out[2 * i] = v;
+  out[2 * i + 1] = make_float4(v.y, v.x, v.w, v.z);
+}
+
+extern "C" int mb_pattern(void* st, void* pcg, void* t, void* obs, void* serving, void* reward,
+                          void* done, int E, int U, void* stream) {
+  const int G = 64 / U;
+  const int waves = (E + G - 1) / G;
+  hipLaunchKernelGGL(k_pattern, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     (int4*)st, (uint64_t*)pcg, (int*)t, (float4*)obs, (int*)serving,
+                     (float*)reward, (uint8_t*)done, E, U);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mb_stream(const void* in, void* out, size_t n, void* stream) {
+  hipLaunchKernelGGL(k_stream, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float4*)in, (float4*)out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,58 @@
+"""Dev tool: memory floor of the step's access pattern vs the real kernel (same process)."""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mobile-env-gan_amd"))
+SO = os.path.join(ROOT, "mobile-env-gan_amd", "lib", "libmembench.so")
+
+
+def timeit(fn, n=100):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+    return t[len(t) // 2]
+
+
+def main():
+    L = C.CDLL(SO)
+    E, U = 65536, 30
+    dev = torch.device("cuda")
+    st = torch.zeros((E, U, 4), dtype=torch.int32, device=dev)
+    pcg = torch.zeros((E, 6), dtype=torch.int64, device=dev)
+    t = torch.zeros(E, dtype=torch.int32, device=dev)
+    obs = torch.zeros((E, U, 4), dtype=torch.float32, device=dev)
+    srv = torch.zeros((E, U), dtype=torch.int32, device=dev)
+    rew = torch.zeros(E, dtype=torch.float32, device=dev)
+    done = torch.zeros(E, dtype=torch.uint8, device=dev)
+    s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda x: C.c_void_p(x.data_ptr())
+    algo = E * (54 * U + 61)
+    us = timeit(lambda: L.mb_pattern(p(st), p(pcg), p(t), p(obs), p(srv), p(rew), p(done), E, U, s()))
+    print(json.dumps({"kernel": "pattern", "us": us, "algo_GBs": algo / us / 1e3}))
+    n = (E * U * 16 + E * 36) // 16  # read bytes / 16
+    a = torch.zeros(n * 4, dtype=torch.float32, device=dev)
+    b = torch.zeros(n * 8, dtype=torch.float32, device=dev)
+    us = timeit(lambda: L.mb_stream(p(a), p(b), C.c_size_t(n), s()))
+    print(json.dumps({"kernel": "stream1r2w", "us": us, "bytes": n * 48, "GBs": n * 48 / us / 1e3}))
+    n2 = 64 << 20
+    a = torch.zeros(n2 * 4, dtype=torch.float32, device=dev)
+    b = torch.zeros(n2 * 8, dtype=torch.float32, device=dev)
+    us = timeit(lambda: L.mb_stream(p(a), p(b), C.c_size_t(n2), s()), 30)
+    print(json.dumps({"kernel": "stream1r2w_3GB", "us": us, "GBs": n2 * 48 / us / 1e3}))
+
+
+if __name__ == "__main__":
+    main()

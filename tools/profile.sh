@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 profile of bench.py's step kernel (run on the GPU box from the repo root):
+#   1. --kernel-trace --stats              -> per-kernel average duration
+#   2. --pmc FETCH_SIZE                    (own pass)
+#   3. --pmc WRITE_SIZE                    (own pass)
+#   4. --pmc SQ_* occupancy/issue counters (own pass)
+# Counters run in separate passes with --kernel-trace only (no sys/runtime tracing).
+# Then tools/pmc_summary.py writes profiles/<tag>_*.csv|md and profiles/pmc_traffic.json.
+# usage: tools/profile.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-r01}; shift
+ARGS="--profile-run --steps 200 --warmup 20 $*"
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # name, extra rocprof args
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS > $OUT/$name.log 2>&1 \
+    || { echo "rocprofv3 $name failed"; tail -20 $OUT/$name.log; return 1; }
+}
+run kt --kernel-trace --stats &&
+run fetch --kernel-trace --pmc FETCH_SIZE &&
+run write --kernel-trace --pmc WRITE_SIZE &&
+run sq --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY &&
+run sq2 --kernel-trace --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE SQ_INST_CYCLES_VMEM_RD &&
+python3 tools/pmc_summary.py $OUT $TAG "$*"
