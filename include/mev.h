@@ -29,7 +29,8 @@
  *                                 seeding (movement re-seeds each episode,
  *                                 movement.py:16-18 with reset_rng_episode=True)
  *       t       int32 [E]         episode time (base.py:175,280)
- *       bs_xy   int32 [B][2] (shared) or [E][B][2] (per env)
+ *       bs_xy   int32 [B][2] (shared; the step kernel uses the keys derived from it by
+ *                                 mev_reset / mev_update_stations) or [E][B][2] (per env)
  *       bs_count int32 [E]        per-env number of valid BSs (NULL: all B)
  *     outputs
  *       obs     f32  [E][U][4]    {x/W, y/H, data rate, scaled utility}
@@ -134,6 +135,11 @@ int mev_seed_pcg64(const uint64_t* seeds, int64_t n, uint64_t* pcg_rows);
  * Writes obs (positions, rate 0, utility 0), serving = -1. */
 int mev_reset(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
               const uint8_t* env_mask, void* stream);
+
+/* Shared station layout (bs_per_env = 0): (re)derive the association keys the step kernel
+ * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the
+ * shared layout between resets. No-op for per-env layouts. Stream-ordered. */
+int mev_update_stations(const mev_ctx* ctx, const int32_t* bs_xy, void* stream);
 
 /* Advance every env by `nsteps` steps of MComCore.step (base.py:230-296), one
  * fused kernel launch per step. An env whose episode is over (t >= min(EP_MAX_TIME,

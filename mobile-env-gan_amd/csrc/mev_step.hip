@@ -48,7 +48,7 @@ namespace {
 constexpr int kMaxU = 1024;
 constexpr int kMaxB = 1024;
 constexpr int kKeyBits = 10;
-constexpr int kMaxSharedBS = 1024;  // shared-layout stations staged in LDS (8 KB)  // BS index bits in the packed (d2, bs) association key
+// (d2, bs) association key: BS index in the low kKeyBits bits
 
 struct KParams {
   int E, U, B, W, H;
@@ -63,6 +63,7 @@ struct KParams {
   float inv_w, inv_h; // obs normalisation
   int d2snap;         // largest integer d2 with sqrt(d2) <= velocity (arrival test)
   float move_band;    // tie band of the float32 movement fast path
+  float u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale, u_offset;  // float32 utility
   int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
   float vel_f;
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
@@ -90,7 +91,7 @@ struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
   const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
-  const double* c100;       // [U + 1]: 100.0 / n  (fast path of the share rounding)
+  const int2* bs_keys;      // [B] shared layout: association keys of the stations
 };
 
 // ------------------------------------------------------------------------------------
@@ -243,14 +244,19 @@ __device__ __forceinline__ double scaled_utility(double rate, const KParams& kp)
 
 // ResourceFair share of the full-rate entry and numpy round(., 2) (base.py:435): the
 // reference value is cents = rint(fl(fl(full / n) * 100)), rate = cents / 100. The fast path
-// forms c = full * fl(100 / n) (within 2^-51 relative of the exact product) and rounds it
+// forms c = full * (100 / n) (within 2^-50 relative of the exact product) and rounds it
 // directly; only when c lies within 2^-46 relative of a half-integer are the two exact
 // float64 operations evaluated. Returns cents (an integer-valued double).
-__device__ __forceinline__ double share_cents(double full, int n, const double* __restrict__ c100) {
-  const double c = full * c100[n];
+__device__ __forceinline__ double share_cents(double full, int n) {
+  // 100 / n to within 2 ulp: hardware reciprocal + two Newton steps (no table, no division)
+  const double dn = (double)n;
+  double r = __builtin_amdgcn_rcp(dn);
+  r = fma(r, fma(-dn, r, 1.0), r);
+  r = fma(r, fma(-dn, r, 1.0), r);
+  const double c = full * (100.0 * r);
   const double f = c - floor(c);
   if (fabs(f - 0.5) > c * 0x1p-46) return rint(c);
-  return rint((full / (double)n) * 100.0);
+  return rint((full / dn) * 100.0);
 }
 
 // Scaled utility of a rounded rate. The utility depends on the rate only, and the rate is
@@ -281,6 +287,17 @@ __device__ __forceinline__ double seg_sum(double v, bool take, int U, int u) {
   return x;
 }
 
+// Float32 form of the scaled BoundedLogUtility (used when no float64 utility output is
+// requested): clip(w1 log(w2 + r) / log(w3), lower, upper) with log via v_log_f32, then the
+// affine scale to [-1, 1]. Relative error ~1e-7 of the float64 value.
+__device__ __forceinline__ double utility_f32(double cents, const KParams& kp) {
+  if (cents <= 0.0) return -1.0;  // rate <= 0 -> lower -> scaled -1
+  const float r = (float)cents * 0.01f;
+  float ur = kp.u_log2_coef * __log2f(kp.u_w2f + r);
+  ur = fminf(fmaxf(ur, kp.u_lowerf), kp.u_upperf);
+  return (double)(ur * kp.u_scale + kp.u_offset);
+}
+
 // ------------------------------------------------------------------------------------
 // Packed shape: U <= 64, G = floor(64/U) envs per wavefront, one lane per UE.
 // ------------------------------------------------------------------------------------
@@ -300,12 +317,13 @@ __device__ __forceinline__ LaneMap lane_map(int lane, int U) {
   return m;
 }
 
-// Per-lane inputs of one env group that are prefetched one group ahead of use. The loads
-// are unconditional (index clamped to a valid env): a guarded load would make the compiler
-// wait for it at the merge point, which defeats the prefetch.
+// Per-lane inputs of one env group (the persistent kernel loads them one group ahead). The
+// loads are unconditional (env index clamped): a guarded load would make the compiler wait
+// for it at the merge point.
 struct GroupIn {
   int t;
-  int4 s;  // {x, y, wx, wy}
+  int4 s;              // {x, y, wx, wy}
+  ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
 };
 
 __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st, int e, int u) {
@@ -313,6 +331,9 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   GroupIn g;
   g.t = st.t[ec];
   g.s = st.ue_state[(size_t)ec * kp.U + u];
+  const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * ec);
+  g.pa = pr[0];
+  g.pb = pr[1];
   return g;
 }
 
@@ -353,29 +374,23 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
 }
 
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
-template <bool PER_ENV_BS>
-__device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
+template <bool PER_ENV_BS, bool PREFETCH>
+__device__ __forceinline__ GroupIn packed_group(const KParams& kp, const KState& st,
                                                 const KOut& out, const KTables& tb,
                                                 const LaneMap& m, const GroupIn& cur, int e,
-                                                bool valid,
-                                                const int2* __restrict__ lds_bsm) {
+                                                bool valid, int e_next) {
   const int U = kp.U;
   const int u = m.u;
   const uint64_t segmask = m.segmask, lt = m.lt;
   const bool want_metrics = out.metrics != nullptr;
-  const bool want_rate = out.rate64 != nullptr || want_metrics || kp.util_direct;
-  // PCG64 row of this env: consumed only by waypoint draws, resets and the state update,
-  // so it is loaded here and its latency hides under the association work
-  const ulonglong2* pr =
-      reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * min(e, kp.E - 1));
-  const ulonglong2 pa = pr[0], pb = pr[1];
-
+  const bool exact_util = out.util64 != nullptr || kp.util_direct;
+  const bool want_rate = out.rate64 != nullptr || want_metrics || exact_util;
   const size_t idx = (size_t)e * U + u;
   int t = cur.t;
   int2 pos = make_int2(cur.s.x, cur.s.y);
   int2 wp = make_int2(cur.s.z, cur.s.w);
-  const u128 inc = mk128(pb.x, pb.y);
-  u128 s = mk128(pa.x, pa.y);
+  const u128 inc = mk128(cur.pb.x, cur.pb.y);
+  u128 s = mk128(cur.pa.x, cur.pa.y);
 
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
   const bool do_reset = valid && t >= kp.t_end;
@@ -401,12 +416,15 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const bool need = active && wp.x < 0;
   const uint64_t mneed_w = __ballot(need);
   const uint64_t mneed = mneed_w & segmask;
+  const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
+  u128 s_next = s;
   if (mneed_w) {
     if (need) {
       u128 su = pcg_advance(s, inc, 2 * __popcll(mneed & lt), tb.jump);
       wp.x = pcg_draw_coord(su, inc, kp.Wd);
       wp.y = pcg_draw_coord(su, inc, kp.Hd);
     }
+    if (u == 0 && tot) s_next = pcg_advance(s, inc, 2 * tot, tb.jump);
   }
   if (active) move_ue(pos, wp, kp);
 
@@ -434,19 +452,31 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       }
     }
   } else if (active) {
+    // shared layout: per-station keys {m = (-2qx, -2qy) as int16x2, k = ((|q|^2 + 2^21) << 10)
+    // | j} precomputed by the context; the rows are wave-uniform (scalar loads) and each
+    // station costs one packed dot product and one shift-add on the vector unit
     const int nb = kp.B;
-#pragma unroll 4
+    const int2* __restrict__ keys = tb.bs_keys;
+#pragma unroll 8
     for (int j = 0; j < nb; ++j) {
-      const int2 mc = lds_bsm[j];  // {(-2qx, -2qy) as int16x2, |q|^2 + 2^21}
-      const unsigned ev = (unsigned)__builtin_amdgcn_sdot2(
-          pu, __builtin_bit_cast(s16x2, mc.x), mc.y, false);
-      best = min(best, (ev << kKeyBits) | (unsigned)j);
+      const int2 kk = keys[j];
+      const int dot = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kk.x), 0, true);
+      best = min(best, ((unsigned)dot << kKeyBits) + (unsigned)kk.y);  // -2p.q + |q|^2 + 2^21
     }
   }
   const int d2s = PER_ENV_BS ? (int)(best >> kKeyBits)
                              : (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
   const int srv =
       (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+
+  // full-rate entry of the serving pair, issued before the per-BS count so its latency
+  // overlaps the ballot loop (index clamped: lanes without a server read a valid entry)
+  const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
+
+  // prefetch of the wave's next group, issued after this group's last dependent load
+  // (vmcnt retires in order: a later wait in this iteration must not have to drain it)
+  GroupIn nxt{};
+  if (PREFETCH) nxt = load_group(kp, st, e_next, u);
 
   // ---- 3. n_b of the own serving BS: lanes of the segment with the same index, matched
   //         bit by bit with ballots (no LDS, no atomics) ---------------------------------
@@ -461,9 +491,13 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
 
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
-  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], n, tb.c100);
+  if (srv >= 0) cents = share_cents(full, n);
   if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
-  const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
+  double util = 0.0;
+  if (active) {
+    // exact float64 utility (table) when the caller asks for it, else the float32 form
+    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32(cents, kp);
+  }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
   const uint64_t mact = __ballot(active) & segmask;
@@ -482,9 +516,7 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
     if (u == 0) {
       const double mean_u = nact > 0 ? sum_u / (double)nact : kp.lower;
-      const int tot = __popcll(mneed);
       if (tot || t == 0) {  // the stream moved (draws, or reset): write the new state back
-        const u128 s_next = tot ? pcg_advance(s, inc, 2 * tot, tb.jump) : s;
         *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
             make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
       }
@@ -498,31 +530,50 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       }
     }
   }
-
+  return nxt;
 }
 
-// Step kernel: one env group per wavefront (latency hidden by occupancy: 8 waves/SIMD).
+// Step kernel: one env group per wavefront (latency hidden by occupancy).
 template <bool PER_ENV_BS>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
-                                                              KTables tb, int ngroups) {
-  __shared__ int2 lds_bsm[PER_ENV_BS ? 1 : kMaxSharedBS];
-  if (!PER_ENV_BS) {  // per-station constants of the association dot product
-    for (int i = threadIdx.x; i < kp.B; i += blockDim.x) {
-      const int2 q = st.bs_xy[i];
-      const s16x2 m2 = {(short)(-2 * q.x), (short)(-2 * q.y)};
-      lds_bsm[i] = make_int2(__builtin_bit_cast(int, m2), q.x * q.x + q.y * q.y + (1 << 21));
-    }
-    __syncthreads();
-  }
+                                                             KTables tb, int ngroups) {
   const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
-  const int g = blockIdx.x * kWavesPerBlock + wib;
+  const int g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
   const LaneMap m = lane_map(lane, kp.U);
   const int e = g * kp.envs_per_wave + m.seg;
   const bool valid = (m.seg < kp.envs_per_wave) && (e < kp.E);
   const GroupIn a = load_group(kp, st, e, m.u);
-  packed_group<PER_ENV_BS>(kp, st, out, tb, m, a, e, valid, lds_bsm);
+  packed_group<PER_ENV_BS, false>(kp, st, out, tb, m, a, e, valid, 0);
+}
+
+// Step kernel, persistent: a resident grid whose wavefronts walk groups g, g + nwaves, ...
+// loading each next group while computing the current one (software pipelining). Manual
+// 2x unroll with two register sets, so the prefetched set is never copied.
+template <bool PER_ENV_BS>
+__global__ __launch_bounds__(kPackedBlock) void k_step_persistent(KParams kp, KState st,
+                                                                 KOut out, KTables tb,
+                                                                 int ngroups) {
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * kWavesPerBlock;
+  const int G = kp.envs_per_wave;
+  const LaneMap m = lane_map(lane, kp.U);
+  int g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  int e = g * G + m.seg;
+  bool valid = (m.seg < G) && (e < kp.E);
+  GroupIn a = load_group(kp, st, e, m.u), b;
+  for (; g < ngroups; g += 2 * nwaves) {
+    const int g1 = g + nwaves;
+    const int e1 = g1 * G + m.seg;
+    b = packed_group<PER_ENV_BS, true>(kp, st, out, tb, m, a, e, valid, e1);
+    if (g1 >= ngroups) break;
+    const int g2 = g1 + nwaves;
+    const int e2 = g2 * G + m.seg;
+    const bool valid1 = (m.seg < G) && (e1 < kp.E);
+    a = packed_group<PER_ENV_BS, true>(kp, st, out, tb, m, b, e1, valid1, e2);
+    e = e2;
+    valid = (g2 < ngroups) && (m.seg < G) && (e2 < kp.E);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -653,7 +704,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
 
   // ---- 4. rate + utility -------------------------------------------------------------
   double cents = 0.0, rate = 0.0;
-  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv], tb.c100);
+  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv]);
   if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
   if (active) lds_util[pre_act + __popcll(mact & lt)] = util;
@@ -724,6 +775,17 @@ __global__ void k_util_table(KParams kp, int kmax, double* __restrict__ tab,
   if (k == kmax && v != kp.util_sat) *bad = 1;  // saturation point must lie inside the table
 }
 
+// Association keys of a shared station layout (see the packed kernel's association):
+// {(-2qx, -2qy) as int16x2, ((qx^2 + qy^2 + 2^21) << 10) | j}.
+__global__ void k_station_keys(const int2* __restrict__ bs, int B, int2* __restrict__ keys) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  const int2 q = bs[j];
+  const s16x2 m2 = {(short)(-2 * q.x), (short)(-2 * q.y)};
+  keys[j] = make_int2(__builtin_bit_cast(int, m2),
+                      (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) | (unsigned)j));
+}
+
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
 __global__ void k_jump_table(int kmax, u128* __restrict__ jump) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -758,7 +820,8 @@ struct mev_ctx {
   double* rate_full;
   u128* jump;
   double* util;
-  double* c100;
+  int2* bs_keys;  // [B] association keys of the shared layout (mev_reset / mev_update_stations)
+  int persistent_blocks;  // > 0: persistent packed kernel with this many workgroups
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -837,6 +900,12 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.srv_bits = 0;
   while ((1 << kp.srv_bits) < params->num_bs) ++kp.srv_bits;
   kp.util_sat = 2.0 * (kp.upper - kp.lower) / (kp.upper - kp.lower) - 1.0;
+  kp.u_log2_coef = (float)(kp.w1 * log(2.0) / kp.log_w3);
+  kp.u_w2f = (float)kp.w2;
+  kp.u_lowerf = (float)kp.lower;
+  kp.u_upperf = (float)kp.upper;
+  kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
+  kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
   kp.vel_f = (float)params->velocity;
   kp.move_band = 0x1p-16f * (params->velocity > 1.0 ? (float)params->velocity : 1.0f);
   {  // arrival threshold and axis-parallel exactness (host IEEE float64 == device)
@@ -900,24 +969,14 @@ int mev_create(const mev_params* params, mev_ctx** out) {
                      c->jump);
   MEV_HIP(hipGetLastError());
 
-  // ---- 100 / n for the share rounding fast path ----
-  {
-    const int nmax = params->num_ues;
-    double* h = (double*)malloc(sizeof(double) * (size_t)(nmax + 1));
-    if (!h || hipMalloc(&c->c100, sizeof(double) * (size_t)(nmax + 1)) != hipSuccess) {
-      free(h);
-      (void)hipFree(c->rate_full);
-      (void)hipFree(c->jump);
-      delete c;
-      return MEV_ENOMEM;
-    }
-    h[0] = 0.0;
-    for (int n = 1; n <= nmax; ++n) h[n] = 100.0 / (double)n;
-    const hipError_t e = hipMemcpy(c->c100, h, sizeof(double) * (size_t)(nmax + 1),
-                                   hipMemcpyHostToDevice);
-    free(h);
-    MEV_HIP(e);
+  // ---- station keys (filled from the caller's layout by mev_reset / mev_update_stations)
+  if (hipMalloc(&c->bs_keys, sizeof(int2) * (size_t)params->num_bs) != hipSuccess) {
+    (void)hipFree(c->rate_full);
+    (void)hipFree(c->jump);
+    delete c;
+    return MEV_ENOMEM;
   }
+  MEV_HIP(hipMemset(c->bs_keys, 0, sizeof(int2) * (size_t)params->num_bs));
 
   // ---- utility table over rounded rates ----
   c->util = nullptr;
@@ -946,6 +1005,14 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   }
   MEV_HIP(hipDeviceSynchronize());
 
+  {  // packed shape: persistent grid = workgroups per CU x CUs (MEV_PERSISTENT=<per CU>, 0 off)
+    int per_cu = 0;
+    const char* env = getenv("MEV_PERSISTENT");
+    if (env) per_cu = atoi(env);
+    hipDeviceProp_t prop;
+    MEV_HIP(hipGetDeviceProperties(&prop, c->device));
+    c->persistent_blocks = per_cu > 0 ? per_cu * prop.multiProcessorCount : 0;
+  }
   *out = c;
   return MEV_OK;
 }
@@ -955,7 +1022,7 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->rate_full);
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
-  (void)hipFree(c->c100);
+  (void)hipFree(c->bs_keys);
   delete c;
 }
 
@@ -997,7 +1064,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util, c->c100};
+  KTables tb{c->rate_full, c->jump, c->util, c->bs_keys};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
@@ -1009,12 +1076,21 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
     } else {
       // persistent: at most c->resident_blocks workgroups, each wave walks several groups
       const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-      if (per_env)
+      if (c->persistent_blocks > 0 && blocks > c->persistent_blocks) {
+        const dim3 grid((unsigned)c->persistent_blocks);
+        if (per_env)
+          hipLaunchKernelGGL((k_step_persistent<true>), grid, dim3(kPackedBlock), 0, stream, kp,
+                             ks, ko, tb, groups);
+        else
+          hipLaunchKernelGGL((k_step_persistent<false>), grid, dim3(kPackedBlock), 0, stream, kp,
+                             ks, ko, tb, groups);
+      } else if (per_env) {
         hipLaunchKernelGGL((k_step_packed<true>), dim3(blocks), dim3(kPackedBlock), 0, stream,
                            kp, ks, ko, tb, groups);
-      else
+      } else {
         hipLaunchKernelGGL((k_step_packed<false>), dim3(blocks), dim3(kPackedBlock), 0, stream,
                            kp, ks, ko, tb, groups);
+      }
     }
   } else {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
@@ -1029,9 +1105,21 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   return MEV_OK;
 }
 
+int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
+  if (!c || !bs_xy) return MEV_EINVAL;
+  if (c->p.bs_per_env) return MEV_OK;  // per-env layouts are read directly by the kernel
+  const int B = c->p.num_bs;
+  hipLaunchKernelGGL(k_station_keys, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const int2*>(bs_xy), B, c->bs_keys);
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
 int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
               const uint8_t* env_mask, void* stream) {
   int rc = check_bufs(c, st, out);
+  if (rc) return rc;
+  rc = mev_update_stations(c, st->bs_xy, stream);
   if (rc) return rc;
   return launch<true>(c, st, out, env_mask, (hipStream_t)stream);
 }

@@ -126,6 +126,9 @@ class StepEngine:
             self.metrics = torch.zeros((E, 4), dtype=torch.float32, **kw) if metrics else None
         self.seed(seeds)
         self._bind()
+        with torch.cuda.device(device):
+            N.check(L.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),
+                    "mev_update_stations")
 
     # -- plumbing -----------------------------------------------------------------------------
     def _bind(self):
@@ -178,6 +181,9 @@ class StepEngine:
         if tuple(bs.shape) != tuple(self.bs_xy.shape):
             raise ValueError("layout shape mismatch")
         self.bs_xy.copy_(bs)
+        with torch.cuda.device(self.device):  # shared layout: re-derive the station keys
+            N.check(self._lib.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),
+                    "mev_update_stations")
         if bs_count is not None:
             if self.bs_count is None:
                 raise ValueError("engine was built without bs_count")

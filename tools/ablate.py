@@ -15,11 +15,20 @@ EDITS = {
     "no_pairwise": [("  const double sum_u = seg_sum(util, active, U, u);",
                      "  const double sum_u = util;")],
     "no_move": [("  if (active) move_ue(pos, wp, kp);\n\n  // ---- 2.", "\n  // ---- 2.")],
-    "no_rate": [("  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], n, tb.c100);",
+    "no_match": [("  for (int bit = 0; bit < kp.srv_bits; ++bit) {", "  for (int bit = 0; bit < 0; ++bit) {")],
+    "no_rate": [("  if (srv >= 0) cents = share_cents(full, n, lds_c100);",
                  "  if (srv >= 0) cents = (double)(d2s * n);")],
-    "no_util": [("  const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;\n\n  // ---- 5.",
-                 "  const double util = active ? cents * 1e-3 : 0.0;\n\n  // ---- 5.")],
+    "no_util": [("    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32(cents, kp);",
+                 "    util = cents * 1e-3;")],
 }
+COMPUTE_ONLY = [
+    ("  g.t = st.t[ec];\n  g.s = st.ue_state[(size_t)ec * kp.U + u];",
+     "  g.t = (ec * 7) % 20;\n  g.s = make_int4((ec * 13 + u * 7) % 200, (ec * 3 + u * 11) % 200, (ec + u) % 200, (ec * 5 + u) % 200);"),
+    ("  const ulonglong2 pa = pr[0], pb = pr[1];",
+     "  const ulonglong2 pa = make_ulonglong2((uint64_t)pr, 7), pb = make_ulonglong2(2 * e + 1, 3);"),
+    ("  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid) {",
+     "  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid && kp.E < 0) {"),
+]
 
 
 def build(name, edits):
@@ -44,4 +53,8 @@ if __name__ == "__main__":
         build(n, EDITS[n])
         allx += EDITS[n]
     build("all", allx)
-    print("built", names + ["all"])
+    build("compute_only", COMPUTE_ONLY)
+    for n in names:
+        build("co_" + n, COMPUTE_ONLY + EDITS[n])
+    build("co_all", COMPUTE_ONLY + allx)
+    print("built", names + ["all", "compute_only"])
