@@ -317,9 +317,8 @@ __device__ __forceinline__ LaneMap lane_map(int lane, int U) {
   return m;
 }
 
-// Per-lane inputs of one env group (the persistent kernel loads them one group ahead). The
-// loads are unconditional (env index clamped): a guarded load would make the compiler wait
-// for it at the merge point.
+// Per-lane inputs of one env group. The loads are unconditional (env index clamped to a
+// valid env): a guarded load would make the compiler wait for it at the merge point.
 struct GroupIn {
   int t;
   int4 s;              // {x, y, wx, wy}
@@ -374,11 +373,11 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
 }
 
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
-template <bool PER_ENV_BS, bool PREFETCH>
-__device__ __forceinline__ GroupIn packed_group(const KParams& kp, const KState& st,
-                                                const KOut& out, const KTables& tb,
-                                                const LaneMap& m, const GroupIn& cur, int e,
-                                                bool valid, int e_next) {
+template <bool PER_ENV_BS>
+__device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
+                                             const KOut& out, const KTables& tb,
+                                             const LaneMap& m, const GroupIn& cur, int e,
+                                             bool valid) {
   const int U = kp.U;
   const int u = m.u;
   const uint64_t segmask = m.segmask, lt = m.lt;
@@ -473,11 +472,6 @@ __device__ __forceinline__ GroupIn packed_group(const KParams& kp, const KState&
   // overlaps the ballot loop (index clamped: lanes without a server read a valid entry)
   const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
 
-  // prefetch of the wave's next group, issued after this group's last dependent load
-  // (vmcnt retires in order: a later wait in this iteration must not have to drain it)
-  GroupIn nxt{};
-  if (PREFETCH) nxt = load_group(kp, st, e_next, u);
-
   // ---- 3. n_b of the own serving BS: lanes of the segment with the same index, matched
   //         bit by bit with ballots (no LDS, no atomics) ---------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
@@ -530,7 +524,6 @@ __device__ __forceinline__ GroupIn packed_group(const KParams& kp, const KState&
       }
     }
   }
-  return nxt;
 }
 
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
@@ -544,36 +537,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const int e = g * kp.envs_per_wave + m.seg;
   const bool valid = (m.seg < kp.envs_per_wave) && (e < kp.E);
   const GroupIn a = load_group(kp, st, e, m.u);
-  packed_group<PER_ENV_BS, false>(kp, st, out, tb, m, a, e, valid, 0);
-}
-
-// Step kernel, persistent: a resident grid whose wavefronts walk groups g, g + nwaves, ...
-// loading each next group while computing the current one (software pipelining). Manual
-// 2x unroll with two register sets, so the prefetched set is never copied.
-template <bool PER_ENV_BS>
-__global__ __launch_bounds__(kPackedBlock) void k_step_persistent(KParams kp, KState st,
-                                                                 KOut out, KTables tb,
-                                                                 int ngroups) {
-  const int lane = threadIdx.x & 63;
-  const int nwaves = gridDim.x * kWavesPerBlock;
-  const int G = kp.envs_per_wave;
-  const LaneMap m = lane_map(lane, kp.U);
-  int g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  int e = g * G + m.seg;
-  bool valid = (m.seg < G) && (e < kp.E);
-  GroupIn a = load_group(kp, st, e, m.u), b;
-  for (; g < ngroups; g += 2 * nwaves) {
-    const int g1 = g + nwaves;
-    const int e1 = g1 * G + m.seg;
-    b = packed_group<PER_ENV_BS, true>(kp, st, out, tb, m, a, e, valid, e1);
-    if (g1 >= ngroups) break;
-    const int g2 = g1 + nwaves;
-    const int e2 = g2 * G + m.seg;
-    const bool valid1 = (m.seg < G) && (e1 < kp.E);
-    a = packed_group<PER_ENV_BS, true>(kp, st, out, tb, m, b, e1, valid1, e2);
-    e = e2;
-    valid = (g2 < ngroups) && (m.seg < G) && (e2 < kp.E);
-  }
+  packed_group<PER_ENV_BS>(kp, st, out, tb, m, a, e, valid);
 }
 
 // ------------------------------------------------------------------------------------
@@ -821,7 +785,6 @@ struct mev_ctx {
   u128* jump;
   double* util;
   int2* bs_keys;  // [B] association keys of the shared layout (mev_reset / mev_update_stations)
-  int persistent_blocks;  // > 0: persistent packed kernel with this many workgroups
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -1005,14 +968,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   }
   MEV_HIP(hipDeviceSynchronize());
 
-  {  // packed shape: persistent grid = workgroups per CU x CUs (MEV_PERSISTENT=<per CU>, 0 off)
-    int per_cu = 0;
-    const char* env = getenv("MEV_PERSISTENT");
-    if (env) per_cu = atoi(env);
-    hipDeviceProp_t prop;
-    MEV_HIP(hipGetDeviceProperties(&prop, c->device));
-    c->persistent_blocks = per_cu > 0 ? per_cu * prop.multiProcessorCount : 0;
-  }
   *out = c;
   return MEV_OK;
 }
@@ -1074,23 +1029,13 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
       hipLaunchKernelGGL(k_reset_packed, grid, dim3(kPackedBlock), 0, stream, kp, ks, ko, tb,
                          mask);
     } else {
-      // persistent: at most c->resident_blocks workgroups, each wave walks several groups
       const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-      if (c->persistent_blocks > 0 && blocks > c->persistent_blocks) {
-        const dim3 grid((unsigned)c->persistent_blocks);
-        if (per_env)
-          hipLaunchKernelGGL((k_step_persistent<true>), grid, dim3(kPackedBlock), 0, stream, kp,
-                             ks, ko, tb, groups);
-        else
-          hipLaunchKernelGGL((k_step_persistent<false>), grid, dim3(kPackedBlock), 0, stream, kp,
-                             ks, ko, tb, groups);
-      } else if (per_env) {
-        hipLaunchKernelGGL((k_step_packed<true>), dim3(blocks), dim3(kPackedBlock), 0, stream,
-                           kp, ks, ko, tb, groups);
-      } else {
+      if (per_env)
+        hipLaunchKernelGGL((k_step_packed<true>), dim3(blocks), dim3(kPackedBlock), 0, stream, kp,
+                           ks, ko, tb, groups);
+      else
         hipLaunchKernelGGL((k_step_packed<false>), dim3(blocks), dim3(kPackedBlock), 0, stream,
                            kp, ks, ko, tb, groups);
-      }
     }
   } else {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
