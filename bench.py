@@ -124,8 +124,11 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
+    from mobile_env.sharding import gather_final, shard_seeds
+
     E = args.envs
-    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=1000 + rank * E)
+    seeds = shard_seeds(1000, E, rank)  # rank r owns global envs [r*E, (r+1)*E)
+    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]))
     U, B = env.num_ues, env.num_bs
     per_env_bs = env.engine.bs_per_env
     env.reset()
@@ -137,9 +140,7 @@ def main():
     stream = torch.cuda.current_stream(device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K)]
-    gather = None
     if world > 1:
-        gather = torch.empty((world, 2, E), dtype=torch.float32, device=device)
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -148,8 +149,7 @@ def main():
         env.step()
         ev[k][1].record(stream)
     if world > 1:  # the one collective: final (reward, done) batch to every rank
-        rd = torch.stack([env.engine.reward, env.engine.done.float()])
-        dist.all_gather_into_tensor(gather, rd)
+        gather_final(env.engine.reward, env.engine.done)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
