@@ -118,11 +118,18 @@ def main():
 
     import mobile_env
 
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one process per GPU over RCCL; on a box with fewer GPUs than ranks (rehearsal only) the
+    # ranks share devices and fall back to gloo (RCCL refuses two ranks on one GPU)
+    ndev = max(1, torch.cuda.device_count())
+    device = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        backend = os.environ.get("MEV_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     from mobile_env.sharding import gather_final, shard_seeds
 
@@ -157,7 +164,8 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

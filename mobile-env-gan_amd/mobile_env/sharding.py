@@ -30,6 +30,8 @@ def gather_final(reward, done, group=None):
     import torch.distributed as dist
 
     rd = torch.stack([reward.float(), done.float()])
+    if dist.get_backend(group) == "gloo":  # CPU rehearsal backend
+        rd = rd.cpu()
     world = dist.get_world_size(group)
     parts = [torch.empty_like(rd) for _ in range(world)]
     dist.all_gather(parts, rd, group=group)
@@ -42,6 +44,8 @@ def gather_obs(obs, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        obs = obs.cpu()
     parts = [torch.empty_like(obs) for _ in range(world)]
     dist.all_gather(parts, obs.contiguous(), group=group)
     return torch.stack(parts)
