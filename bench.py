@@ -13,8 +13,9 @@ Contract (see DESIGN.md "Measurement"):
   (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
   ranks time. Inputs are resident in HBM before timing starts.
 * roofline: algorithmic bytes per launch = E * (54*U + 61) over the kernel's
-  average duration, measured with HIP events recorded around every launch on the stream the
-  kernel runs on. traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
+  average duration, measured with HIP events on the stream the kernel runs on, recorded
+  around every chunk of 20 back-to-back launches (the average includes the gaps between
+  launches). traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
   (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
@@ -143,18 +144,22 @@ def main():
         env.step()
     torch.cuda.synchronize(device)
 
-    K = args.steps
+    # Steps are issued in chunks of CHUNK back-to-back launches from C (mev_step loops over
+    # launches; a Python call per step would make the host, not the GPU, the bottleneck),
+    # with a HIP event pair around every chunk on the kernel's stream.
+    CHUNK = 20
+    K = -(-args.steps // CHUNK) * CHUNK
     stream = torch.cuda.current_stream(device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+          for _ in range(K // CHUNK)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for k in range(K):
-        ev[k][0].record(stream)
-        env.step()
-        ev[k][1].record(stream)
+    for a, b in ev:
+        a.record(stream)
+        env.engine.step(CHUNK)
+        b.record(stream)
     if world > 1:  # the one collective: final (reward, done) batch to every rank
         gather_final(env.engine.reward, env.engine.done)
     torch.cuda.synchronize(device)

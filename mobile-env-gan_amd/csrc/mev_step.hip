@@ -127,6 +127,23 @@ __device__ __forceinline__ int pcg_draw_coord(u128& s, u128 inc, double span) {
   return (int)(0.0 + span * d);
 }
 
+// The two draws (x then y) of a waypoint / initial position at stream offsets k+1, k+2:
+// jump straight to offset k+1 with the table, then one step with the constant multiplier.
+// Returns the stream state after both draws.
+__device__ __forceinline__ u128 pcg_draw_pair(u128 s, u128 inc, int k, const u128* jump,
+                                              double w, double h, int& x, int& y) {
+  const u128 s1 = jump[2 * (k + 1)] * s + jump[2 * (k + 1) + 1] * inc;
+  x = (int)(0.0 + w * ((double)(pcg_output(s1) >> 11) * (1.0 / 9007199254740992.0)));
+  const u128 s2 = s1 * mk128(PCG_MULT_LO, PCG_MULT_HI) + inc;
+  y = (int)(0.0 + h * ((double)(pcg_output(s2) >> 11) * (1.0 / 9007199254740992.0)));
+  return s2;
+}
+
+__device__ __forceinline__ u128 shfl_u128(u128 v, int src) {
+  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+  return mk128(__shfl(lo, src), __shfl(hi, src));
+}
+
 // numpy pairwise-sum order for n <= 128 (numpy/_core/src/umath/loops_utils.h.src),
 // evaluated by lane 0 of a segment over LDS values a[0..n).
 __device__ __forceinline__ double pairwise_small(const double* a, int n) {
@@ -306,6 +323,8 @@ struct LaneMap {
   uint64_t segmask, lt;
 };
 
+__device__ __forceinline__ int lane_self(const LaneMap& m) { return m.base + m.u; }
+
 __device__ __forceinline__ LaneMap lane_map(int lane, int U) {
   LaneMap m;
   // lane / U through float: (lane + 0.5) / U is >= 0.5/U away from an integer
@@ -394,17 +413,18 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
   const bool do_reset = valid && t >= kp.t_end;
   if (__ballot(do_reset)) {
+    u128 s2 = s;
     if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc =
           reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
       const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : s;
-      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
-      pos.x = pcg_draw_coord(su, inc, kp.Wd);
-      pos.y = pcg_draw_coord(su, inc, kp.Hd);
-      s = pcg_advance(s0, inc, 2 * U, tb.jump);
+      s2 = pcg_draw_pair(s0, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       wp = make_int2(-1, -1);
       t = 0;
     }
+    // the env's stream continues after the last UE's two draws (offset 2U)
+    const u128 s_end = shfl_u128(s2, m.base + U - 1);
+    if (do_reset) s = s_end;
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
@@ -418,12 +438,13 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
   u128 s_next = s;
   if (mneed_w) {
-    if (need) {
-      u128 su = pcg_advance(s, inc, 2 * __popcll(mneed & lt), tb.jump);
-      wp.x = pcg_draw_coord(su, inc, kp.Wd);
-      wp.y = pcg_draw_coord(su, inc, kp.Hd);
-    }
-    if (u == 0 && tot) s_next = pcg_advance(s, inc, 2 * tot, tb.jump);
+    u128 s2 = s;
+    if (need)
+      s2 = pcg_draw_pair(s, inc, 2 * __popcll(mneed & lt), tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
+    // the env's stream continues after the last drawing lane of the segment (offset 2*tot)
+    const int last = tot ? 63 - __clzll((unsigned long long)mneed) : lane_self(m);
+    const u128 s_last = shfl_u128(s2, last);
+    if (tot) s_next = s_last;
   }
   if (active) move_ue(pos, wp, kp);
 

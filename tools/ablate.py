@@ -10,13 +10,13 @@ OUT = os.path.join(ROOT, "mobile-env-gan_amd", "lib")
 
 EDITS = {
     "no_draw": [("  if (mneed_w) {", "  if (false) {")],
-    "no_assoc": [("  } else if (active) {\n    const int nb = kp.B;",
-                  "  } else if (active) {\n    best = (unsigned)(pos.x & 1023) << kKeyBits;\n    const int nb = 0;")],
+    "no_assoc": [("    const int nb = kp.B;\n    const int2* __restrict__ keys",
+                  "    best = (unsigned)(pos.x & 1023) << kKeyBits;\n    const int nb = 0;\n    const int2* __restrict__ keys")],
     "no_pairwise": [("  const double sum_u = seg_sum(util, active, U, u);",
                      "  const double sum_u = util;")],
     "no_move": [("  if (active) move_ue(pos, wp, kp);\n\n  // ---- 2.", "\n  // ---- 2.")],
     "no_match": [("  for (int bit = 0; bit < kp.srv_bits; ++bit) {", "  for (int bit = 0; bit < 0; ++bit) {")],
-    "no_rate": [("  if (srv >= 0) cents = share_cents(full, n, lds_c100);",
+    "no_rate": [("  if (srv >= 0) cents = share_cents(full, n);",
                  "  if (srv >= 0) cents = (double)(d2s * n);")],
     "no_util": [("    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32(cents, kp);",
                  "    util = cents * 1e-3;")],
@@ -24,8 +24,8 @@ EDITS = {
 COMPUTE_ONLY = [
     ("  g.t = st.t[ec];\n  g.s = st.ue_state[(size_t)ec * kp.U + u];",
      "  g.t = (ec * 7) % 20;\n  g.s = make_int4((ec * 13 + u * 7) % 200, (ec * 3 + u * 11) % 200, (ec + u) % 200, (ec * 5 + u) % 200);"),
-    ("  const ulonglong2 pa = pr[0], pb = pr[1];",
-     "  const ulonglong2 pa = make_ulonglong2((uint64_t)pr, 7), pb = make_ulonglong2(2 * e + 1, 3);"),
+    ("  g.pa = pr[0];\n  g.pb = pr[1];",
+     "  g.pa = make_ulonglong2((uint64_t)pr, 7);\n  g.pb = make_ulonglong2(2 * e + 1, 3);"),
     ("  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid) {",
      "  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid && kp.E < 0) {"),
 ]

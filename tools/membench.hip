@@ -42,17 +42,42 @@ __global__ __launch_bounds__(256) void k_stream(const float4* __restrict__ in, f
 }
 
 extern "C" int mb_pattern(void* st, void* pcg, void* t, void* obs, void* serving, void* reward,
-                          void* done, int E, int U, void* stream) {
+                          void* done, int E, int U, int reps, void* stream) {
   const int G = 64 / U;
   const int waves = (E + G - 1) / G;
+  for (int r = 0; r < reps; ++r)
   hipLaunchKernelGGL(k_pattern, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                      (int4*)st, (uint64_t*)pcg, (int*)t, (float4*)obs, (int*)serving,
                      (float*)reward, (uint8_t*)done, E, U);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mb_stream(const void* in, void* out, size_t n, void* stream) {
+extern "C" int mb_stream(const void* in, void* out, size_t n, int reps, void* stream) {
+  for (int r = 0; r < reps; ++r)
   hipLaunchKernelGGL(k_stream, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      (const float4*)in, (float4*)out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// launch-overhead probes: same grid as the step kernel
+__global__ __launch_bounds__(256) void k_empty(int* p) {
+  if (threadIdx.x == 1000) p[0] = 1;
+}
+__global__ __launch_bounds__(256) void k_touch(const int4* __restrict__ st, int* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const int4 v = st[i];
+    if (v.x == 123456789) out[0] = v.y;
+  }
+}
+extern "C" int mb_empty(void* p, int blocks, int reps, void* stream) {
+  for (int r = 0; r < reps; ++r)
+  hipLaunchKernelGGL(k_empty, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (int*)p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int mb_touch(const void* st, void* out, int n, int reps, void* stream) {
+  for (int r = 0; r < reps; ++r)
+  hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const int4*)st, (int*)out, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -17,14 +17,15 @@ def run(name, E, steps=200, vel=None):
     eng = StepEngine(p, L["bs"], 1000, device="cuda")
     eng.step(40)
     torch.cuda.synchronize()
+    reps = 20  # back-to-back launches from the C loop per timed chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+          for _ in range(steps // reps)]
     for a, b in ev:
         a.record()
-        eng.step(1)
+        eng.step(reps)
         b.record()
     torch.cuda.synchronize()
-    t = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+    t = sorted(a.elapsed_time(b) * 1e3 / reps for a, b in ev)
     eng.close()
     U = L["num_ues"]
     return {"scenario": name, "E": E, "vel": p.velocity, "us_mean": sum(t) / len(t),
