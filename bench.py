@@ -93,8 +93,8 @@ def load_traffic(workload: str, envs: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--warmup", type=int, default=2000)
     ap.add_argument("--workload", default="mobile-large-central-v0")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -139,14 +139,20 @@ def main():
     env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]))
     U, B = env.num_ues, env.num_bs
     per_env_bs = env.engine.bs_per_env
+    parts = env.engine.launch_parts
     env.reset()
-    for _ in range(args.warmup):
+    # warmup (also brings the GPU to its steady clock): the Gym step once, then C-loop chunks
+    if args.warmup > 0:
         env.step()
+        env.engine.step(args.warmup - 1)
     torch.cuda.synchronize(device)
 
     # Steps are issued in chunks of CHUNK back-to-back launches from C (mev_step loops over
     # launches; a Python call per step would make the host, not the GPU, the bottleneck),
-    # with a HIP event pair around every chunk on the kernel's stream.
+    # with a HIP event pair around every chunk on the caller's stream. With the two-half
+    # launch shape (mev_params.stream_split) the second half runs on the context's own
+    # stream and is joined back before mev_step returns, so each event pair brackets whole
+    # steps of the full batch.
     CHUNK = 20
     K = -(-args.steps // CHUNK) * CHUNK
     stream = torch.cuda.current_stream(device)
@@ -200,7 +206,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "kernel_ms": kern_ms},
+                         "kernel_ms": kern_ms,
+                         "launch_shape": (f"{parts} halves per step on {parts} HIP streams"
+                                          if parts > 1 else "one kernel per step")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 1
+#define MEV_ABI_VERSION 2
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -76,6 +76,10 @@ typedef struct mev_params {
   int32_t movement_reseed;   /* 1: movement RNG re-seeded every episode (movement_params
                                 reset_rng_episode=True, base.py:133, movement.py:16-18);
                                 0: one stream continued across episodes */
+  int32_t stream_split;      /* mev_step launch shape: 0 auto, 1 one kernel per step on the
+                                caller's stream, 2 the env batch in two halves on the caller's
+                                stream and a context-owned stream (joined before return), so
+                                one half's tail overlaps the other half's start */
   double velocity;        /* UE velocity (base.py:119, custom.py:16-18) */
   double bs_bw, bs_freq, bs_tx, bs_height;        /* base.py:117 */
   double ue_snr_tr, ue_noise, ue_height;          /* base.py:118-123 */
@@ -117,6 +121,8 @@ void mev_destroy(mev_ctx* ctx);
 
 /* Largest connectable squared distance (snr > snr_tr <=> d2 <= d2max); -1 if none. */
 int mev_d2max(const mev_ctx* ctx);
+/* Number of env halves mev_step launches per step (1, or 2 on two streams; stream_split). */
+int mev_launch_parts(const mev_ctx* ctx);
 /* Device pointer to the channel rate table (float64 [d2max+1]) -- for tests. */
 const double* mev_rate_table(const mev_ctx* ctx);
 /* Copy the first n entries of the channel rate table to dst (host or device memory,

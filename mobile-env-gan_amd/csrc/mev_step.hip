@@ -344,11 +344,12 @@ struct GroupIn {
   ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
 };
 
-__device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st, int e, int u) {
+__device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st, int e, int u,
+                                              int U) {
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   g.t = st.t[ec];
-  g.s = st.ue_state[(size_t)ec * kp.U + u];
+  g.s = st.ue_state[(size_t)ec * U + u];
   const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * ec);
   g.pa = pr[0];
   g.pb = pr[1];
@@ -392,17 +393,21 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
 }
 
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
-template <bool PER_ENV_BS>
+//   UC:   U as a compile-time constant (0: runtime kp.U) -- folds the lane map, the segment
+//         reductions and the env indexing for the registered scenario sizes;
+//   LEAN: no float64 rate / utility / metrics outputs and the utility in its float32 form
+//         (the Gym surface's default), so none of the optional work is even branched over.
+template <bool PER_ENV_BS, bool LEAN, int UC>
 __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, const GroupIn& cur, int e,
                                              bool valid) {
-  const int U = kp.U;
+  const int U = UC ? UC : kp.U;
   const int u = m.u;
   const uint64_t segmask = m.segmask, lt = m.lt;
-  const bool want_metrics = out.metrics != nullptr;
-  const bool exact_util = out.util64 != nullptr || kp.util_direct;
-  const bool want_rate = out.rate64 != nullptr || want_metrics || exact_util;
+  const bool want_metrics = !LEAN && out.metrics != nullptr;
+  const bool exact_util = !LEAN && (out.util64 != nullptr || kp.util_direct);
+  const bool want_rate = !LEAN && (out.rate64 != nullptr || want_metrics || exact_util);
   const size_t idx = (size_t)e * U + u;
   int t = cur.t;
   int2 pos = make_int2(cur.s.x, cur.s.y);
@@ -527,10 +532,14 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     out.serving[idx] = srv;
     out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
                                (float)cents * 0.01f, (float)util);
-    if (out.rate64) out.rate64[idx] = rate;
-    if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
+    if (!LEAN && out.rate64) out.rate64[idx] = rate;
+    if (!LEAN && out.util64) out.util64[idx] = active ? util : __builtin_nan("");
     if (u == 0) {
-      const double mean_u = nact > 0 ? sum_u / (double)nact : kp.lower;
+      // np.mean; the lean path divides in float32 (the reward output is float32)
+      const double mean_u =
+          LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
+                           : kp.lower)
+               : (nact > 0 ? sum_u / (double)nact : kp.lower);
       if (tot || t == 0) {  // the stream moved (draws, or reset): write the new state back
         *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
             make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
@@ -548,17 +557,20 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
 }
 
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
-template <bool PER_ENV_BS>
+// Groups [g0, ngroups) of the batch (g0 > 0: second half of the two-stream shape).
+template <bool PER_ENV_BS, bool LEAN, int UC>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
-                                                             KTables tb, int ngroups) {
+                                                             KTables tb, int g0, int ngroups) {
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int g = g0 + blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
-  const LaneMap m = lane_map(lane, kp.U);
-  const int e = g * kp.envs_per_wave + m.seg;
-  const bool valid = (m.seg < kp.envs_per_wave) && (e < kp.E);
-  const GroupIn a = load_group(kp, st, e, m.u);
-  packed_group<PER_ENV_BS>(kp, st, out, tb, m, a, e, valid);
+  const int U = UC ? UC : kp.U;
+  const int G = UC ? 64 / UC : kp.envs_per_wave;
+  const LaneMap m = lane_map(lane, U);
+  const int e = g * G + m.seg;
+  const bool valid = (m.seg < G) && (e < kp.E);
+  const GroupIn a = load_group(kp, st, e, m.u, U);
+  packed_group<PER_ENV_BS, LEAN, UC>(kp, st, out, tb, m, a, e, valid);
 }
 
 // ------------------------------------------------------------------------------------
@@ -806,6 +818,9 @@ struct mev_ctx {
   u128* jump;
   double* util;
   int2* bs_keys;  // [B] association keys of the shared layout (mev_reset / mev_update_stations)
+  int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
+  hipStream_t aux;    // second stream of the two-half shape
+  hipEvent_t ev_fork, ev_join;
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -843,6 +858,7 @@ static int validate(const mev_params* p) {
   if (p->num_bs < 1 || p->num_bs > kMaxB) return MEV_EINVAL;
   if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
   if (p->ep_max_time < 1 || p->arrival_exit < 1) return MEV_EINVAL;
+  if (p->stream_split < 0 || p->stream_split > 2) return MEV_EINVAL;
   if (!(p->velocity >= 0.0) || !(p->ue_noise > 0.0) || !(p->util_upper > p->util_lower))
     return MEV_EINVAL;
   return MEV_OK;
@@ -987,6 +1003,18 @@ int mev_create(const mev_params* params, mev_ctx** out) {
       c->kp.util_direct = 1;
     }
   }
+  // ---- launch shape of mev_step: two halves on two streams when each half still fills
+  //      the chip several times over (>= 4096 wavefronts per half)
+  c->parts = 1;
+  if (c->kp.U <= 64) {
+    const int groups = (c->kp.E + c->kp.envs_per_wave - 1) / c->kp.envs_per_wave;
+    c->parts = params->stream_split ? params->stream_split : (groups >= 8192 ? 2 : 1);
+  }
+  if (c->parts == 2) {
+    MEV_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    MEV_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    MEV_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+  }
   MEV_HIP(hipDeviceSynchronize());
 
   *out = c;
@@ -999,10 +1027,15 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
   (void)hipFree(c->bs_keys);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   delete c;
 }
 
 int mev_d2max(const mev_ctx* c) { return c ? c->d2max : MEV_EINVAL; }
+
+int mev_launch_parts(const mev_ctx* c) { return c ? c->parts : MEV_EINVAL; }
 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 
@@ -1034,6 +1067,55 @@ static void to_kernel(const mev_state* st, const mev_outputs* out, KState& ks, K
   ko.metrics = reinterpret_cast<float4*>(out->metrics);
 }
 
+typedef void (*StepKernel)(KParams, KState, KOut, KTables, int, int);
+
+template <bool PER_ENV_BS, bool LEAN>
+static StepKernel step_kernel_u(int U) {
+  switch (U) {  // scenario sizes of the registry (small / medium / large)
+    case 5: return k_step_packed<PER_ENV_BS, LEAN, 5>;
+    case 15: return k_step_packed<PER_ENV_BS, LEAN, 15>;
+    case 30: return k_step_packed<PER_ENV_BS, LEAN, 30>;
+    default: return k_step_packed<PER_ENV_BS, LEAN, 0>;
+  }
+}
+
+static StepKernel step_kernel_for(bool per_env, bool lean, int U) {
+  if (per_env) return lean ? step_kernel_u<true, true>(U) : step_kernel_u<true, false>(U);
+  return lean ? step_kernel_u<false, true>(U) : step_kernel_u<false, false>(U);
+}
+
+// Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
+// the caller's stream, the second on c->aux (forked from and joined back into the caller's
+// stream); the halves are independent envs, so the two streams overlap freely.
+static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& ko,
+                               const KTables& tb, int nsteps, hipStream_t stream) {
+  const KParams& kp = c->kp;
+  const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
+  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !kp.util_direct;
+  const StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
+  // split on a block boundary
+  const int half = (groups / 2 + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+  if (c->parts == 1 || half <= 0 || half >= groups) {
+    const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    for (int i = 0; i < nsteps; ++i)
+      k<<<dim3(blocks), dim3(kPackedBlock), 0, stream>>>(kp, ks, ko, tb, 0, groups);
+    MEV_HIP(hipGetLastError());
+    return MEV_OK;
+  }
+  const int blocks0 = half / kWavesPerBlock;
+  const int blocks1 = (groups - half + kWavesPerBlock - 1) / kWavesPerBlock;
+  MEV_HIP(hipEventRecord(c->ev_fork, stream));
+  MEV_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  for (int i = 0; i < nsteps; ++i) {
+    k<<<dim3(blocks0), dim3(kPackedBlock), 0, stream>>>(kp, ks, ko, tb, 0, half);
+    k<<<dim3(blocks1), dim3(kPackedBlock), 0, c->aux>>>(kp, ks, ko, tb, half, groups);
+  }
+  MEV_HIP(hipGetLastError());
+  MEV_HIP(hipEventRecord(c->ev_join, c->aux));
+  MEV_HIP(hipStreamWaitEvent(stream, c->ev_join, 0));
+  return MEV_OK;
+}
+
 template <bool RESET>
 static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
                   const uint8_t* mask, hipStream_t stream) {
@@ -1050,13 +1132,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
       hipLaunchKernelGGL(k_reset_packed, grid, dim3(kPackedBlock), 0, stream, kp, ks, ko, tb,
                          mask);
     } else {
-      const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-      if (per_env)
-        hipLaunchKernelGGL((k_step_packed<true>), dim3(blocks), dim3(kPackedBlock), 0, stream, kp,
-                           ks, ko, tb, groups);
-      else
-        hipLaunchKernelGGL((k_step_packed<false>), dim3(blocks), dim3(kPackedBlock), 0, stream,
-                           kp, ks, ko, tb, groups);
+      return launch_packed_steps(c, ks, ko, tb, 1, stream);
     }
   } else {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
@@ -1095,6 +1171,13 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   if (nsteps < 0) return MEV_EINVAL;
+  if (c->kp.U <= 64) {
+    KState ks;
+    KOut ko;
+    to_kernel(st, out, ks, ko);
+    const KTables tb{c->rate_full, c->jump, c->util, c->bs_keys};
+    return launch_packed_steps(c, ks, ko, tb, nsteps, (hipStream_t)stream);
+  }
   for (int i = 0; i < nsteps; ++i) {
     rc = launch<false>(c, st, out, nullptr, (hipStream_t)stream);
     if (rc) return rc;

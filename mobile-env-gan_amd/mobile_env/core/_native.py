@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -22,8 +22,9 @@ MEV_EHIP = -1000
 MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
-EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_rate_table",
-           "mev_copy_rate_table", "mev_seed_pcg64", "mev_update_stations", "mev_reset", "mev_step", "mev_strerror", "mev_last_hip_error")
+EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts",
+           "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_update_stations",
+           "mev_reset", "mev_step", "mev_strerror", "mev_last_hip_error")
 
 
 class MevParams(C.Structure):
@@ -32,7 +33,7 @@ class MevParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("ep_max_time", C.c_int32),
         ("arrival_start", C.c_int32), ("arrival_exit", C.c_int32),
         ("bs_per_env", C.c_int32), ("first_step_active", C.c_int32),
-        ("movement_reseed", C.c_int32),
+        ("movement_reseed", C.c_int32), ("stream_split", C.c_int32),
         ("velocity", C.c_double),
         ("bs_bw", C.c_double), ("bs_freq", C.c_double), ("bs_tx", C.c_double),
         ("bs_height", C.c_double),
@@ -84,6 +85,8 @@ def lib():
         L.mev_destroy.restype = None
         L.mev_d2max.argtypes = [C.c_void_p]
         L.mev_d2max.restype = C.c_int
+        L.mev_launch_parts.argtypes = [C.c_void_p]
+        L.mev_launch_parts.restype = C.c_int
         L.mev_rate_table.argtypes = [C.c_void_p]
         L.mev_rate_table.restype = C.c_void_p
         L.mev_copy_rate_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]

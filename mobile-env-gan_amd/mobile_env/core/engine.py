@@ -50,6 +50,7 @@ class EngineParams:
     util_lower: float = -20.0
     util_upper: float = 20.0
     util_coeffs: tuple = (10.0, 0.0, 10.0)
+    stream_split: int = 0  # mev_params.stream_split: 0 auto, 1 single stream, 2 two halves
 
     def to_c(self, bs_per_env: bool) -> N.MevParams:
         return N.MevParams(
@@ -58,6 +59,7 @@ class EngineParams:
             arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
             bs_per_env=int(bs_per_env), first_step_active=int(bool(self.first_step_active)),
             movement_reseed=int(bool(self.movement_reseed)),
+            stream_split=int(self.stream_split),
             velocity=float(self.velocity),
             bs_bw=float(self.bs["bw"]), bs_freq=float(self.bs["freq"]),
             bs_tx=float(self.bs["tx"]), bs_height=float(self.bs["height"]),
@@ -154,6 +156,11 @@ class StepEngine:
     @property
     def d2max(self) -> int:
         return int(self._lib.mev_d2max(self._ctx))
+
+    @property
+    def launch_parts(self) -> int:
+        """Env halves per step launch (1, or 2 on two streams)."""
+        return int(self._lib.mev_launch_parts(self._ctx))
 
     def rate_table(self):
         """Host copy (numpy float64) of the device-built channel table rate_full[0..d2max]."""

@@ -81,7 +81,7 @@ def test_create_rejects_bad_params_without_gpu():
     from mobile_env.core.engine import EngineParams
     lib = N.lib()
     for bad in (dict(num_envs=0), dict(num_ues=0), dict(num_ues=1025), dict(num_bs=0),
-                dict(width=2000)):
+                dict(width=2000), dict(stream_split=3)):
         kw = dict(num_envs=4, num_ues=5, num_bs=3)
         kw.update(bad)
         cp = EngineParams(**kw).to_c(False)

@@ -21,7 +21,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-STEP_RE = re.compile(r"k_step_packed1?<(true|false)>|k_step_block<(true|false), false>")
+STEP_RE = re.compile(r"k_step_packed<|k_step_block<(true|false), false>")
 
 
 def is_step_kernel(name: str) -> bool:
@@ -37,6 +37,23 @@ def counters(path_glob):
                     continue
                 vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def step_interval(trace_glob, steps):
+    """From the kernel trace: step-kernel dispatches of the timed region (the last
+    steps x parts), their average duration, and the step interval = (last end - first start)
+    / steps -- with two halves per step on two streams the dispatch durations overlap, so
+    the interval, not the duration, is the time of a step."""
+    rows = []
+    for path in glob.glob(trace_glob, recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if is_step_kernel(row.get("Kernel_Name", "")):
+                    rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    if not rows or not steps:
+        return None
+    rows.sort()
+    return rows, steps
 
 
 def main():
@@ -58,20 +75,38 @@ def main():
         v, n = counters(os.path.join(out, name, "**", "*counter_collection.csv"))
         pmc.update(v)
         ndisp.update(n)
-    workload, envs = "mobile-large-central-v0", 65536
+    workload, envs, steps, warmup = "mobile-large-central-v0", 65536, 0, 0
     toks = extra.split()
     for i, t in enumerate(toks):
         if t == "--workload":
             workload = toks[i + 1]
         if t == "--envs":
             envs = int(toks[i + 1])
+        if t == "--steps":
+            steps = int(toks[i + 1])
+        if t == "--warmup":
+            warmup = int(toks[i + 1])
     summary = {"tag": tag, "workload": workload, "envs": envs, "bench_args": extra,
                "step_kernel_avg_ns": step_avg_ns, "counters_per_launch": pmc,
                "dispatches_sampled": ndisp}
+    tr = step_interval(os.path.join(out, "kt", "**", "*kernel_trace.csv"), steps)
+    parts = 1
+    if tr:
+        rows, _ = tr
+        total_steps = steps + warmup
+        parts = max(1, round(len(rows) / total_steps))
+        timed = rows[-steps * parts:]
+        span = max(e for _, e in timed) - timed[0][0]
+        summary["launch_parts"] = parts
+        summary["timed_dispatches"] = len(timed)
+        summary["timed_dispatch_avg_ns"] = sum(e - b for b, e in timed) / len(timed)
+        summary["step_interval_ns"] = span / steps
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-        fetch = pmc["FETCH_SIZE"] * 1024 * 2
-        write = pmc["WRITE_SIZE"] * 1024
+        # per step = per dispatch x halves per step (the halves are equal-sized)
+        fetch = pmc["FETCH_SIZE"] * 1024 * 2 * parts
+        write = pmc["WRITE_SIZE"] * 1024 * parts
         summary["hbm_bytes_per_launch"] = fetch + write
+        summary["hbm_bytes_per_step"] = fetch + write
         summary["fetch_bytes_per_launch_corrected"] = fetch
         summary["write_bytes_per_launch"] = write
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:

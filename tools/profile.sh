@@ -5,11 +5,12 @@
 #   3. --pmc WRITE_SIZE                    (own pass)
 #   4. --pmc SQ_* occupancy/issue counters (own pass)
 # Counters run in separate passes with --kernel-trace only (no sys/runtime tracing).
-# Then tools/pmc_summary.py writes profiles/<tag>_*.csv|md and profiles/pmc_traffic.json.
+# Then, locally after the merge: python tools/pmc_summary.py gpurun_out/prof_TAG TAG "<ARGS>"
+# writes profiles/<tag>_*.csv/json and profiles/pmc_traffic.json.
 # usage: tools/profile.sh TAG [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
-ARGS="--profile-run --steps 200 --warmup 20 $*"
+ARGS="--profile-run --steps 1000 --warmup 1000 $*"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -23,4 +24,4 @@ run fetch --kernel-trace --pmc FETCH_SIZE &&
 run write --kernel-trace --pmc WRITE_SIZE &&
 run sq --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY &&
 run sq2 --kernel-trace --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE SQ_INST_CYCLES_VMEM_RD &&
-python3 tools/pmc_summary.py $OUT $TAG "$*"
+echo "profile done: $OUT"

@@ -13,7 +13,8 @@ from mobile_env.scenarios.registry import LAYOUTS  # noqa: E402
 def run(name, E, steps=200, vel=None):
     L = LAYOUTS[name]
     p = EngineParams(num_envs=E, num_ues=L["num_ues"], num_bs=len(L["bs"]),
-                     velocity=vel if vel is not None else 1.5)
+                     velocity=vel if vel is not None else 1.5,
+                     stream_split=int(os.environ.get("MEV_VB_SPLIT", "0")))
     eng = StepEngine(p, L["bs"], 1000, device="cuda")
     eng.step(40)
     torch.cuda.synchronize()
@@ -33,7 +34,8 @@ def run(name, E, steps=200, vel=None):
 
 
 if __name__ == "__main__":
-    tag = os.environ.get("TAG", os.environ.get("MEV_LIB", "default"))
+    tag = os.environ.get("TAG", os.environ.get("MEV_LIB", "default")) + \
+        " split=" + os.environ.get("MEV_VB_SPLIT", "0")
     cases = (("large", 65536), ("large", 65536, 200, 10.0), ("medium", 4096), ("small", 65536))
     for args in cases[:int(os.environ.get("MEV_VB_CASES", len(cases)))]:
         r = run(*args)
