@@ -66,6 +66,7 @@ struct KParams {
   float u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale, u_offset;  // float32 utility
   int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
   float vel_f;
+  int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
 };
 
@@ -556,13 +557,26 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   }
 }
 
+// Block -> env-range slot. Blocks are dealt round-robin over the 8 XCDs (observed placement,
+// MI355X_MICROARCH.md "Workgroup dispatch"); with the remap the blocks that share an XCD
+// (equal blockIdx % 8) cover one contiguous range, so the per-env rows that several blocks
+// write partially (t, reward, done, pcg) are merged in one L2 instead of eight. Bijective
+// for any grid size. Speed only: any block order is correct.
+__device__ __forceinline__ int block_slot(int remap) {
+  const int orig = blockIdx.x;
+  if (!remap) return orig;
+  const int nwg = gridDim.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
 // Groups [g0, ngroups) of the batch (g0 > 0: second half of the two-stream shape).
 template <bool PER_ENV_BS, bool LEAN, int UC>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb, int g0, int ngroups) {
   const int lane = threadIdx.x & 63;
-  const int g = g0 + blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int g = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
   const int U = UC ? UC : kp.U;
   const int G = UC ? 64 / UC : kp.envs_per_wave;
@@ -907,6 +921,10 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
   kp.vel_f = (float)params->velocity;
+  {
+    const char* xr = getenv("MEV_XCD_REMAP");  // dev A/B switch
+    kp.xcd_remap = xr ? atoi(xr) : 1;
+  }
   kp.move_band = 0x1p-16f * (params->velocity > 1.0 ? (float)params->velocity : 1.0f);
   {  // arrival threshold and axis-parallel exactness (host IEEE float64 == device)
     const int d2_top = (params->width - 1) * (params->width - 1) +

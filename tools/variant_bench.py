@@ -16,7 +16,7 @@ def run(name, E, steps=200, vel=None):
                      velocity=vel if vel is not None else 1.5,
                      stream_split=int(os.environ.get("MEV_VB_SPLIT", "0")))
     eng = StepEngine(p, L["bs"], 1000, device="cuda")
-    eng.step(40)
+    eng.step(int(os.environ.get("MEV_VB_WARMUP", "3000")))  # to steady GPU clocks
     torch.cuda.synchronize()
     reps = 20  # back-to-back launches from the C loop per timed chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
