@@ -20,7 +20,7 @@
  *     `stream` (NULL = default stream). A context is not thread-safe; use one
  *     context per (device, stream).
  *   - Layout (SoA, row-major, E envs, U UEs, B base stations per env):
- *       ue_state int32 [E][U][4]  {x, y, wx, wy}: UE position (integer grid,
+ *       ue_state int16 [E][U][4]  {x, y, wx, wy}: UE position (integer grid,
  *                                 entities.py:52-54) and RandomWaypoint target
  *                                 (movement.py:44-47); wx < 0 means "no waypoint"
  *       pcg     uint64[E][6]      numpy-PCG64 stream of the movement model:
@@ -30,7 +30,8 @@
  *                                 movement.py:16-18 with reset_rng_episode=True)
  *       t       int32 [E]         episode time (base.py:175,280)
  *       bs_xy   int32 [B][2] (shared; the step kernel uses the keys derived from it by
- *                                 mev_reset / mev_update_stations) or [E][B][2] (per env)
+ *                                 mev_reset / mev_update_stations) or [E][B][2] (per env);
+ *                                 coordinates in [0, 1024)
  *       bs_count int32 [E]        per-env number of valid BSs (NULL: all B)
  *     outputs
  *       obs     f32  [E][U][4]    {x/W, y/H, data rate, scaled utility}
@@ -51,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 2
+#define MEV_ABI_VERSION 3
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -88,7 +89,7 @@ typedef struct mev_params {
 } mev_params;
 
 typedef struct mev_state {
-  int32_t* ue_state;
+  int16_t* ue_state;
   uint64_t* pcg;
   int32_t* t;
   const int32_t* bs_xy;

@@ -71,7 +71,7 @@ struct KParams {
 };
 
 struct KState {
-  int4* ue_state;  // [E][U] {x, y, wx, wy}
+  int2* ue_state;  // [E][U] {x, y, wx, wy} as int16x4 (8 B per UE; coordinates < 1024, -1)
   uint64_t* pcg;
   int* t;
   const int2* bs_xy;
@@ -94,6 +94,17 @@ struct KTables {
   const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
   const int2* bs_keys;      // [B] shared layout: association keys of the stations
 };
+
+// UE state row {x, y, wx, wy} packed as int16x4: one 8-byte load / store per UE.
+__device__ __forceinline__ int4 load_ue(const int2* p) {
+  const int2 v = *p;
+  return make_int4((int)(short)v.x, v.x >> 16, (int)(short)v.y, v.y >> 16);
+}
+
+__device__ __forceinline__ void store_ue(int2* p, int2 pos, int2 wp) {
+  *p = make_int2((int)(((unsigned)pos.x & 0xffffu) | ((unsigned)pos.y << 16)),
+                 (int)(((unsigned)wp.x & 0xffffu) | ((unsigned)wp.y << 16)));
+}
 
 // ------------------------------------------------------------------------------------
 // PCG64 helpers (device)
@@ -350,7 +361,7 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   g.t = st.t[ec];
-  g.s = st.ue_state[(size_t)ec * U + u];
+  g.s = load_ue(st.ue_state + (size_t)ec * U + u);
   const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * ec);
   g.pa = pr[0];
   g.pb = pr[1];
@@ -377,7 +388,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
   const int x = pcg_draw_coord(su, inc, kp.Wd);
   const int y = pcg_draw_coord(su, inc, kp.Hd);
   const size_t idx = (size_t)e * kp.U + m.u;
-  st.ue_state[idx] = make_int4(x, y, -1, -1);
+  store_ue(st.ue_state + idx, make_int2(x, y), make_int2(-1, -1));
   out.serving[idx] = -1;
   out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
   if (out.rate64) out.rate64[idx] = 0.0;
@@ -483,11 +494,21 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     // station costs one packed dot product and one shift-add on the vector unit
     const int nb = kp.B;
     const int2* __restrict__ keys = tb.bs_keys;
+    if (keys[nb].x) {  // format 1 (wave-uniform): one dot product with accumulator per station
+      const s16x2 pu32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
 #pragma unroll 8
-    for (int j = 0; j < nb; ++j) {
-      const int2 kk = keys[j];
-      const int dot = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kk.x), 0, true);
-      best = min(best, ((unsigned)dot << kKeyBits) + (unsigned)kk.y);  // -2p.q + |q|^2 + 2^21
+      for (int j = 0; j < nb; ++j) {
+        const int2 kk = keys[j];
+        best = min(best, (unsigned)__builtin_amdgcn_sdot2(pu32, __builtin_bit_cast(s16x2, kk.x),
+                                                          kk.y, false));
+      }
+    } else {
+#pragma unroll 8
+      for (int j = 0; j < nb; ++j) {
+        const int2 kk = keys[j];
+        const int dot = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kk.x), 0, true);
+        best = min(best, ((unsigned)dot << kKeyBits) + (unsigned)kk.y);  // -2p.q + |q|^2 + 2^21
+      }
     }
   }
   const int d2s = PER_ENV_BS ? (int)(best >> kKeyBits)
@@ -529,7 +550,7 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
 
   // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
-    st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
+    store_ue(st.ue_state + idx, pos, wp);
     out.serving[idx] = srv;
     out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
                                (float)cents * 0.01f, (float)util);
@@ -631,7 +652,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   } else {
     s = mk128(a.x, a.y);
     if (valid) {
-      const int4 sv = st.ue_state[idx];
+      const int4 sv = load_ue(st.ue_state + idx);
       pos = make_int2(sv.x, sv.y);
       wp = make_int2(sv.z, sv.w);
     }
@@ -639,7 +660,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
 
   if (RESET) {
     if (valid) {
-      st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
+      store_ue(st.ue_state + idx, pos, wp);
       out.serving[idx] = -1;
       out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
       if (out.rate64) out.rate64[idx] = 0.0;
@@ -724,7 +745,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   __syncthreads();
 
   if (valid) {
-    st.ue_state[idx] = make_int4(pos.x, pos.y, wp.x, wp.y);
+    store_ue(st.ue_state + idx, pos, wp);
     out.serving[idx] = srv;
     out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
                                (float)cents * 0.01f, (float)util);
@@ -787,14 +808,26 @@ __global__ void k_util_table(KParams kp, int kmax, double* __restrict__ tab,
 }
 
 // Association keys of a shared station layout (see the packed kernel's association):
-// {(-2qx, -2qy) as int16x2, ((qx^2 + qy^2 + 2^21) << 10) | j}.
-__global__ void k_station_keys(const int2* __restrict__ bs, int B, int2* __restrict__ keys) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= B) return;
-  const int2 q = bs[j];
-  const s16x2 m2 = {(short)(-2 * q.x), (short)(-2 * q.y)};
-  keys[j] = make_int2(__builtin_bit_cast(int, m2),
-                      (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) | (unsigned)j));
+// keys[j] = {m_j as int16x2, c_j = ((qx^2 + qy^2 + 2^21) << 10) | j}, keys[B].x = format.
+//   format 1 (map <= 512 x 512 and every station in [0, 512)^2): m_j = (-64 qx, -64 qy); the
+//     kernel forms the key as ONE dot product with accumulator, dot2((32 px, 32 py), m_j) +
+//     c_j = ((|q|^2 + 2^21 - 2 p.q) << 10) | j (all terms fit int16, the key fits 32 bits);
+//   format 0: m_j = (-2 qx, -2 qy), key = (dot2(p, m_j) << 10) + c_j.
+// One workgroup (B <= 1024).
+__global__ __launch_bounds__(1024) void k_station_keys(const int2* __restrict__ bs, int B, int W,
+                                                       int H, int2* __restrict__ keys) {
+  const int j = threadIdx.x;
+  const int2 q = j < B ? bs[j] : make_int2(0, 0);
+  const bool in = q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
+  const bool scaled = __syncthreads_and(j >= B || in) && W <= 512 && H <= 512;
+  if (j < B) {
+    const int f = scaled ? -64 : -2;
+    const s16x2 m2 = {(short)(f * q.x), (short)(f * q.y)};
+    keys[j] = make_int2(__builtin_bit_cast(int, m2),
+                        (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) |
+                              (unsigned)j));
+  }
+  if (j == 0) keys[B] = make_int2(scaled ? 1 : 0, 0);
 }
 
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
@@ -988,13 +1021,13 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   MEV_HIP(hipGetLastError());
 
   // ---- station keys (filled from the caller's layout by mev_reset / mev_update_stations)
-  if (hipMalloc(&c->bs_keys, sizeof(int2) * (size_t)params->num_bs) != hipSuccess) {
+  if (hipMalloc(&c->bs_keys, sizeof(int2) * (size_t)(params->num_bs + 1)) != hipSuccess) {
     (void)hipFree(c->rate_full);
     (void)hipFree(c->jump);
     delete c;
     return MEV_ENOMEM;
   }
-  MEV_HIP(hipMemset(c->bs_keys, 0, sizeof(int2) * (size_t)params->num_bs));
+  MEV_HIP(hipMemset(c->bs_keys, 0, sizeof(int2) * (size_t)(params->num_bs + 1)));
 
   // ---- utility table over rounded rates ----
   c->util = nullptr;
@@ -1071,7 +1104,7 @@ static int check_bufs(const mev_ctx* c, const mev_state* st, const mev_outputs* 
 }
 
 static void to_kernel(const mev_state* st, const mev_outputs* out, KState& ks, KOut& ko) {
-  ks.ue_state = reinterpret_cast<int4*>(st->ue_state);
+  ks.ue_state = reinterpret_cast<int2*>(st->ue_state);
   ks.pcg = st->pcg;
   ks.t = st->t;
   ks.bs_xy = reinterpret_cast<const int2*>(st->bs_xy);
@@ -1169,8 +1202,9 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   if (!c || !bs_xy) return MEV_EINVAL;
   if (c->p.bs_per_env) return MEV_OK;  // per-env layouts are read directly by the kernel
   const int B = c->p.num_bs;
-  hipLaunchKernelGGL(k_station_keys, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const int2*>(bs_xy), B, c->bs_keys);
+  hipLaunchKernelGGL(k_station_keys, dim3(1), dim3(1024), 0, (hipStream_t)stream,
+                     reinterpret_cast<const int2*>(bs_xy), B, c->p.width, c->p.height,
+                     c->bs_keys);
   MEV_HIP(hipGetLastError());
   return MEV_OK;
 }

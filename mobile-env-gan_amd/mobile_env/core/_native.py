@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12

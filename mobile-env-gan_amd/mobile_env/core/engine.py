@@ -9,7 +9,7 @@ reference keeps in entity/plugin objects:
 tensor                 reference state                      reference file:line
 =====================  ===================================  ============================
 ``ue_state [E,U,4]``   ``UserEquipment.x/.y`` (cols 0-1)    entities.py:47-48, base.py:233
-  ``i32``              ``RandomWaypointMovement``           movement.py:33,44-47,55
+  ``i16``              ``RandomWaypointMovement``           movement.py:33,44-47,55
                        ``.userMoveDirection`` (cols 2-3,
                        wx<0: none)
 ``pcg [E,6] u64``      ``Movement.rng`` (numpy PCG64)       movement.py:16-18
@@ -74,6 +74,17 @@ class EngineParams:
         return min(int(self.ep_max_time), int(self.arrival_exit))
 
 
+def _check_station_range(bs, bs_count=None):
+    """Station coordinates must lie in [0, 1024) (mev.h: the association keys are 32-bit);
+    per-env layouts with a station count: only the first bs_count[e] rows are stations."""
+    if bs_count is not None and bs.dim() == 3:
+        cnt = torch.as_tensor(bs_count, dtype=torch.int64, device=bs.device).reshape(-1, 1)
+        keep = torch.arange(bs.shape[1], device=bs.device)[None, :] < cnt
+        bs = bs[keep]
+    if bs.numel() and (int(bs.min()) < 0 or int(bs.max()) > 1023):
+        raise ValueError("base-station coordinates must lie in [0, 1024)")
+
+
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(None)
 
@@ -102,6 +113,7 @@ class StepEngine:
         B = bs.shape[-2]
         if B != params.num_bs:
             raise ValueError(f"bs_xy has {B} stations, params say {params.num_bs}")
+        _check_station_range(bs, bs_count)
         L = N.lib()
         with torch.cuda.device(device):
             cp = params.to_c(self.bs_per_env)
@@ -116,7 +128,7 @@ class StepEngine:
                 self.bs_count = torch.as_tensor(bs_count, dtype=torch.int32).reshape(E).to(**kw)
                 if int(self.bs_count.max()) > B or int(self.bs_count.min()) < 0:
                     raise ValueError("bs_count out of range")
-            self.ue_state = torch.full((E, U, 4), -1, dtype=torch.int32, **kw)
+            self.ue_state = torch.full((E, U, 4), -1, dtype=torch.int16, **kw)
             self.t = torch.full((E,), params.t_end, dtype=torch.int32, **kw)
             self.pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
             self.obs = torch.zeros((E, U, 4), dtype=torch.float32, **kw)
@@ -187,6 +199,7 @@ class StepEngine:
         bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)
         if tuple(bs.shape) != tuple(self.bs_xy.shape):
             raise ValueError("layout shape mismatch")
+        _check_station_range(bs, bs_count)
         self.bs_xy.copy_(bs)
         with torch.cuda.device(self.device):  # shared layout: re-derive the station keys
             N.check(self._lib.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),

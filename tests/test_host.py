@@ -168,3 +168,18 @@ def test_engine_refuses_cpu_device():
     with pytest.raises(RuntimeError):
         StepEngine(EngineParams(num_envs=1, num_ues=5, num_bs=3), [[0, 0]] * 3, [1],
                    device="cpu")
+
+
+def test_station_range_check():
+    import torch
+    from mobile_env.core.engine import _check_station_range
+    _check_station_range(torch.tensor([[0, 0], [1023, 5]]))
+    with pytest.raises(ValueError):
+        _check_station_range(torch.tensor([[0, 0], [1024, 5]]))
+    with pytest.raises(ValueError):
+        _check_station_range(torch.tensor([[-1, 0]]))
+    # per-env layouts: rows beyond bs_count are padding and are not checked
+    lay = torch.tensor([[[5, 5], [-1, -1]], [[7, 7], [8, 8]]])
+    _check_station_range(lay, [1, 2])
+    with pytest.raises(ValueError):
+        _check_station_range(lay, [2, 2])

@@ -22,7 +22,7 @@ EDITS = {
                  "    util = cents * 1e-3;")],
 }
 COMPUTE_ONLY = [
-    ("  g.t = st.t[ec];\n  g.s = st.ue_state[(size_t)ec * kp.U + u];",
+    ("  g.t = st.t[ec];\n  g.s = st.ue_state[(size_t)ec * U + u];",
      "  g.t = (ec * 7) % 20;\n  g.s = make_int4((ec * 13 + u * 7) % 200, (ec * 3 + u * 11) % 200, (ec + u) % 200, (ec * 5 + u) % 200);"),
     ("  g.pa = pr[0];\n  g.pb = pr[1];",
      "  g.pa = make_ulonglong2((uint64_t)pr, 7);\n  g.pb = make_ulonglong2(2 * e + 1, 3);"),

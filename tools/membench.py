@@ -15,7 +15,7 @@ SO = os.path.join(ROOT, "mobile-env-gan_amd", "lib", "libmembench.so")
 def timeit(fn, n=100, reps=20):
     """Median over n chunks of `reps` back-to-back launches issued from C (the host loop
     never starves the GPU), per launch."""
-    fn(10)
+    fn(2000)  # to steady GPU clocks
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     for a, b in ev:
