@@ -92,7 +92,7 @@ struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
   const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
-  const int2* bs_keys;      // [B] shared layout: association keys of the stations
+  const int4* assoc;        // [H][W] shared layout: {serving BS or -1, d2, full rate (f64)}
 };
 
 // UE state row {x, y, wx, wy} packed as int16x4: one 8-byte load / store per UE.
@@ -151,9 +151,15 @@ __device__ __forceinline__ u128 pcg_draw_pair(u128 s, u128 inc, int k, const u12
   return s2;
 }
 
-__device__ __forceinline__ u128 shfl_u128(u128 v, int src) {
-  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
-  return mk128(__shfl(lo, src), __shfl(hi, src));
+// The same pair at stream offsets 1, 2 (two steps of the constant multiplier).
+__device__ __forceinline__ u128 pcg_draw_pair_next(u128 s, u128 inc, double w, double h, int& x,
+                                                   int& y) {
+  const u128 a = mk128(PCG_MULT_LO, PCG_MULT_HI);
+  const u128 s1 = s * a + inc;
+  x = (int)(0.0 + w * ((double)(pcg_output(s1) >> 11) * (1.0 / 9007199254740992.0)));
+  const u128 s2 = s1 * a + inc;
+  y = (int)(0.0 + h * ((double)(pcg_output(s2) >> 11) * (1.0 / 9007199254740992.0)));
+  return s2;
 }
 
 // numpy pairwise-sum order for n <= 128 (numpy/_core/src/umath/loops_utils.h.src),
@@ -335,8 +341,6 @@ struct LaneMap {
   uint64_t segmask, lt;
 };
 
-__device__ __forceinline__ int lane_self(const LaneMap& m) { return m.base + m.u; }
-
 __device__ __forceinline__ LaneMap lane_map(int lane, int U) {
   LaneMap m;
   // lane / U through float: (lane + 0.5) / U is >= 0.5/U away from an integer
@@ -427,21 +431,25 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const u128 inc = mk128(cur.pb.x, cur.pb.y);
   u128 s = mk128(cur.pa.x, cur.pa.y);
 
+  // Stream bookkeeping without cross-lane moves: the step's waypoint draws start at offset
+  // koff of stream state `s` (koff = 2U right after a reset: the initial positions took the
+  // first 2U draws), and the lane that made the env's LAST draw of the step writes the new
+  // stream state back.
+  int koff = 0;
+  u128 s_fin = s;  // stream state after this lane's last draw
+
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
   const bool do_reset = valid && t >= kp.t_end;
   if (__ballot(do_reset)) {
-    u128 s2 = s;
     if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc =
           reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
-      const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : s;
-      s2 = pcg_draw_pair(s0, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+      if (kp.movement_reseed) s = mk128(pc.x, pc.y);
+      s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+      koff = 2 * U;
       wp = make_int2(-1, -1);
       t = 0;
     }
-    // the env's stream continues after the last UE's two draws (offset 2U)
-    const u128 s_end = shfl_u128(s2, m.base + U - 1);
-    if (do_reset) s = s_end;
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
@@ -453,26 +461,29 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const uint64_t mneed_w = __ballot(need);
   const uint64_t mneed = mneed_w & segmask;
   const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
-  u128 s_next = s;
+  const int rank = __popcll(mneed & lt);
   if (mneed_w) {
-    u128 s2 = s;
-    if (need)
-      s2 = pcg_draw_pair(s, inc, 2 * __popcll(mneed & lt), tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
-    // the env's stream continues after the last drawing lane of the segment (offset 2*tot)
-    const int last = tot ? 63 - __clzll((unsigned long long)mneed) : lane_self(m);
-    const u128 s_last = shfl_u128(s2, last);
-    if (tot) s_next = s_last;
+    // common case: every drawing lane of the wave is the first of its env and no reset came
+    // before -> two steps of the constant multiplier instead of a table jump
+    if (__ballot(need && (rank | koff)) == 0) {
+      if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, wp.x, wp.y);
+    } else {
+      if (need) s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
+    }
   }
+  // owner of the env's new stream state: the last drawing lane, else (reset without draws)
+  // the last UE's lane, else nobody (the stream did not move)
+  const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
   if (active) move_ue(pos, wp, kp);
 
   // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
-  // key = (e << 10) | j, min over stations j: ties keep the lower index (python min() over
-  // the station dict). Shared layout: e = d2 - |p|^2 + 2^21 = |q|^2 + 2^21 - 2 p.q is ONE
-  // packed-int16 dot product per station with the per-station constants from LDS (|p|^2 is
-  // the same for every station, so the argmin is unchanged). Per-env layout: e = d2.
-  unsigned best = UINT_MAX;
-  const s16x2 pu = {(short)pos.x, (short)pos.y};
+  int srv = -1;
+  double full = 0.0;
   if (PER_ENV_BS) {
+    // per-env layout: key = (d2 << 10) | j, min over the env's stations (ties keep the lower
+    // index, as python's min() over the station dict)
+    unsigned best = UINT_MAX;
+    const s16x2 pu = {(short)pos.x, (short)pos.y};
     const int nb = st.bs_count ? (valid ? st.bs_count[e] : 0) : kp.B;
     const int2* bs = st.bs_xy + (size_t)e * kp.B;
     if (active && nb > 0) {
@@ -488,37 +499,22 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
         }
       }
     }
-  } else if (active) {
-    // shared layout: per-station keys {m = (-2qx, -2qy) as int16x2, k = ((|q|^2 + 2^21) << 10)
-    // | j} precomputed by the context; the rows are wave-uniform (scalar loads) and each
-    // station costs one packed dot product and one shift-add on the vector unit
-    const int nb = kp.B;
-    const int2* __restrict__ keys = tb.bs_keys;
-    if (keys[nb].x) {  // format 1 (wave-uniform): one dot product with accumulator per station
-      const s16x2 pu32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
-#pragma unroll 8
-      for (int j = 0; j < nb; ++j) {
-        const int2 kk = keys[j];
-        best = min(best, (unsigned)__builtin_amdgcn_sdot2(pu32, __builtin_bit_cast(s16x2, kk.x),
-                                                          kk.y, false));
-      }
-    } else {
-#pragma unroll 8
-      for (int j = 0; j < nb; ++j) {
-        const int2 kk = keys[j];
-        const int dot = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kk.x), 0, true);
-        best = min(best, ((unsigned)dot << kKeyBits) + (unsigned)kk.y);  // -2p.q + |q|^2 + 2^21
-      }
+    const int d2s = (int)(best >> kKeyBits);
+    if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & ((1u << kKeyBits) - 1));
+    // full-rate entry of the serving pair (index clamped: lanes without a server read a
+    // valid entry)
+    full = tb.rate_full[max(0, min(d2s, kp.d2max))];
+  } else {
+    // shared layout: the association map holds, for every grid position of the map, the
+    // serving station (or -1) and the full rate of that pair -- one 16-byte gather from an
+    // L2-resident table replaces the per-station loop and the rate-table read
+    const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
+    const int4 r = tb.assoc[yi * kp.W + xi];
+    if (active) {
+      srv = r.x;
+      full = __hiloint2double(r.w, r.z);
     }
   }
-  const int d2s = PER_ENV_BS ? (int)(best >> kKeyBits)
-                             : (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
-  const int srv =
-      (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
-
-  // full-rate entry of the serving pair, issued before the per-BS count so its latency
-  // overlaps the ballot loop (index clamped: lanes without a server read a valid entry)
-  const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
 
   // ---- 3. n_b of the own serving BS: lanes of the segment with the same index, matched
   //         bit by bit with ballots (no LDS, no atomics) ---------------------------------
@@ -554,6 +550,9 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     out.serving[idx] = srv;
     out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
                                (float)cents * 0.01f, (float)util);
+    if (own_fin)  // the stream moved (draws, or reset): write the new state back
+      *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+          make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
     if (!LEAN && out.util64) out.util64[idx] = active ? util : __builtin_nan("");
     if (u == 0) {
@@ -562,10 +561,6 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
           LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
                            : kp.lower)
                : (nact > 0 ? sum_u / (double)nact : kp.lower);
-      if (tot || t == 0) {  // the stream moved (draws, or reset): write the new state back
-        *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
-            make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
-      }
       st.t[e] = t + 1;
       out.reward[e] = (float)mean_u;
       out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
@@ -600,7 +595,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const int g = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
   const int U = UC ? UC : kp.U;
-  const int G = UC ? 64 / UC : kp.envs_per_wave;
+  const int G = UC ? 64 / (UC ? UC : 1) : kp.envs_per_wave;
   const LaneMap m = lane_map(lane, U);
   const int e = g * G + m.seg;
   const bool valid = (m.seg < G) && (e < kp.E);
@@ -807,27 +802,32 @@ __global__ void k_util_table(KParams kp, int kmax, double* __restrict__ tab,
   if (k == kmax && v != kp.util_sat) *bad = 1;  // saturation point must lie inside the table
 }
 
-// Association keys of a shared station layout (see the packed kernel's association):
-// keys[j] = {m_j as int16x2, c_j = ((qx^2 + qy^2 + 2^21) << 10) | j}, keys[B].x = format.
-//   format 1 (map <= 512 x 512 and every station in [0, 512)^2): m_j = (-64 qx, -64 qy); the
-//     kernel forms the key as ONE dot product with accumulator, dot2((32 px, 32 py), m_j) +
-//     c_j = ((|q|^2 + 2^21 - 2 p.q) << 10) | j (all terms fit int16, the key fits 32 bits);
-//   format 0: m_j = (-2 qx, -2 qy), key = (dot2(p, m_j) << 10) + c_j.
-// One workgroup (B <= 1024).
-__global__ __launch_bounds__(1024) void k_station_keys(const int2* __restrict__ bs, int B, int W,
-                                                       int H, int2* __restrict__ keys) {
-  const int j = threadIdx.x;
-  const int2 q = j < B ? bs[j] : make_int2(0, 0);
-  const bool in = q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
-  const bool scaled = __syncthreads_and(j >= B || in) && W <= 512 && H <= 512;
-  if (j < B) {
-    const int f = scaled ? -64 : -2;
-    const s16x2 m2 = {(short)(f * q.x), (short)(f * q.y)};
-    keys[j] = make_int2(__builtin_bit_cast(int, m2),
-                        (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) |
-                              (unsigned)j));
+// Association map of a shared station layout: for every grid position (x, y) of the map,
+// {serving station (or -1), d2 to it, full rate rate_full[d2] as float64}. The serving station
+// is the closest one (ties: lower index, python's min() over the station dict) and only if
+// d2 <= d2max (snr > snr_tr, base.py:212-214,236-241). d2 in 64-bit: any int32 coordinates.
+__global__ void k_assoc_map(const int2* __restrict__ bs, int B, int W, int H, int d2max,
+                            const double* __restrict__ rate_full, int4* __restrict__ map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * H) return;
+  const int x = i % W, y = i / W;
+  long long best = LLONG_MAX;
+  int jb = -1;
+  for (int j = 0; j < B; ++j) {
+    const int2 q = bs[j];
+    const long long dx = (long long)x - q.x, dy = (long long)y - q.y;
+    const long long d2 = dx * dx + dy * dy;
+    if (d2 < best) {
+      best = d2;
+      jb = j;
+    }
   }
-  if (j == 0) keys[B] = make_int2(scaled ? 1 : 0, 0);
+  int4 r = make_int4(-1, 0, 0, 0);
+  if (jb >= 0 && best <= d2max) {
+    const double f = rate_full[best];
+    r = make_int4(jb, (int)best, __double2loint(f), __double2hiint(f));
+  }
+  map[i] = r;
 }
 
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
@@ -864,7 +864,7 @@ struct mev_ctx {
   double* rate_full;
   u128* jump;
   double* util;
-  int2* bs_keys;  // [B] association keys of the shared layout (mev_reset / mev_update_stations)
+  int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
   hipStream_t aux;    // second stream of the two-half shape
   hipEvent_t ev_fork, ev_join;
@@ -988,7 +988,8 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   int* d_aux = nullptr;
   if (hipMalloc(&c->rate_full, sizeof(double) * (size_t)(d2_hi + 1)) != hipSuccess ||
       hipMalloc(&d_aux, 2 * sizeof(int)) != hipSuccess) {
-    delete c;
+    if (d_aux) (void)hipFree(d_aux);
+    mev_destroy(c);
     return MEV_ENOMEM;
   }
   const int init_aux[2] = {-1, 0};
@@ -1004,30 +1005,31 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   c->d2max = aux[0];
   c->kp.d2max = c->d2max;
   if (aux[1] != aux[0] + 1) {  // connectable set must be exactly [0, d2max]
-    (void)hipFree(c->rate_full);
-    delete c;
+    mev_destroy(c);
     return MEV_ECHANNEL;
   }
 
   // ---- PCG64 jump table: offsets up to 2U (reset) + 2U (waypoints) ----
   c->jmax = 4 * params->num_ues;
   if (hipMalloc(&c->jump, sizeof(u128) * 2 * (size_t)(c->jmax + 1)) != hipSuccess) {
-    (void)hipFree(c->rate_full);
-    delete c;
+    mev_destroy(c);
     return MEV_ENOMEM;
   }
   hipLaunchKernelGGL(k_jump_table, dim3((c->jmax + 256) / 256), dim3(256), 0, 0, c->jmax,
                      c->jump);
   MEV_HIP(hipGetLastError());
 
-  // ---- station keys (filled from the caller's layout by mev_reset / mev_update_stations)
-  if (hipMalloc(&c->bs_keys, sizeof(int2) * (size_t)(params->num_bs + 1)) != hipSuccess) {
-    (void)hipFree(c->rate_full);
-    (void)hipFree(c->jump);
-    delete c;
-    return MEV_ENOMEM;
+  // ---- association map of a shared layout (filled by mev_reset / mev_update_stations;
+  //      <= 1024 x 1024 x 16 B)
+  c->assoc = nullptr;
+  if (!params->bs_per_env) {
+    const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height;
+    if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
+      mev_destroy(c);
+      return MEV_ENOMEM;
+    }
+    MEV_HIP(hipMemset(c->assoc, 0xff, bytes));  // srv -1 everywhere until a layout is set
   }
-  MEV_HIP(hipMemset(c->bs_keys, 0, sizeof(int2) * (size_t)(params->num_bs + 1)));
 
   // ---- utility table over rounded rates ----
   c->util = nullptr;
@@ -1036,9 +1038,8 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     int* d_bad = nullptr;
     if (hipMalloc(&c->util, sizeof(double) * (size_t)(kmax + 1)) != hipSuccess ||
         hipMalloc(&d_bad, sizeof(int)) != hipSuccess) {
-      (void)hipFree(c->rate_full);
-      (void)hipFree(c->jump);
-      delete c;
+      if (d_bad) (void)hipFree(d_bad);
+      mev_destroy(c);
       return MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(d_bad, 0, sizeof(int)));
@@ -1077,7 +1078,7 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->rate_full);
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
-  (void)hipFree(c->bs_keys);
+  if (c->assoc) (void)hipFree(c->assoc);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1173,7 +1174,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util, c->bs_keys};
+  KTables tb{c->rate_full, c->jump, c->util, c->assoc};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
@@ -1201,10 +1202,10 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
 int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   if (!c || !bs_xy) return MEV_EINVAL;
   if (c->p.bs_per_env) return MEV_OK;  // per-env layouts are read directly by the kernel
-  const int B = c->p.num_bs;
-  hipLaunchKernelGGL(k_station_keys, dim3(1), dim3(1024), 0, (hipStream_t)stream,
-                     reinterpret_cast<const int2*>(bs_xy), B, c->p.width, c->p.height,
-                     c->bs_keys);
+  const int cells = c->p.width * c->p.height;
+  hipLaunchKernelGGL(k_assoc_map, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
+                     c->p.height, c->d2max, c->rate_full, c->assoc);
   MEV_HIP(hipGetLastError());
   return MEV_OK;
 }
@@ -1227,7 +1228,7 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
     KState ks;
     KOut ko;
     to_kernel(st, out, ks, ko);
-    const KTables tb{c->rate_full, c->jump, c->util, c->bs_keys};
+    const KTables tb{c->rate_full, c->jump, c->util, c->assoc};
     return launch_packed_steps(c, ks, ko, tb, nsteps, (hipStream_t)stream);
   }
   for (int i = 0; i < nsteps; ++i) {
