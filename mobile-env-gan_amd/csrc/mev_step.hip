@@ -60,6 +60,7 @@ struct KParams {
   int srv_bits;       // bits of a serving-BS index (ceil(log2(B))), for the ballot match
   int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
   int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
+  int hist_lds;       // packed shape: per-env BS counts in an LDS histogram ([G][B] per wave)
   float inv_w, inv_h; // obs normalisation
   int d2snap;         // largest integer d2 with sqrt(d2) <= velocity (arrival test)
   float move_band;    // tie band of the float32 movement fast path
@@ -322,6 +323,29 @@ __device__ __forceinline__ double seg_sum(double v, bool take, int U, int u) {
   return x;
 }
 
+// float64 DPP move (both halves), invalid source lanes / masked rows read 0.0
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWMASK, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum of `v` over the lanes of an aligned segment of P = 16 or 32 lanes with `take` set
+// (all 64 lanes must be active): row prefix sums by row_shr 1/2/4/8, then (P = 32) the lower
+// row's total added into the upper row by row_bcast15. The result is valid in the segment's
+// last lane (u = P - 1).
+template <int P>
+__device__ __forceinline__ double seg_sum_rows(double v, bool take) {
+  double x = take ? v : 0.0;
+  x += dpp_f64<0x111>(x);  // row_shr:1
+  x += dpp_f64<0x112>(x);  // row_shr:2
+  x += dpp_f64<0x114>(x);  // row_shr:4
+  x += dpp_f64<0x118>(x);  // row_shr:8
+  if (P == 32) x += dpp_f64<0x142, 0xa>(x);  // row_bcast:15 into rows 1 and 3
+  return x;
+}
+
 // Float32 form of the scaled BoundedLogUtility (used when no float64 utility output is
 // requested): clip(w1 log(w2 + r) / log(w3), lower, upper) with log via v_log_f32, then the
 // affine scale to [-1, 1]. Relative error ~1e-7 of the float64 value.
@@ -336,18 +360,32 @@ __device__ __forceinline__ double utility_f32(double cents, const KParams& kp) {
 // ------------------------------------------------------------------------------------
 // Packed shape: U <= 64, G = floor(64/U) envs per wavefront, one lane per UE.
 // ------------------------------------------------------------------------------------
+// An env occupies a segment of P >= U consecutive lanes (the segment pitch): lanes
+// base .. base+U-1 hold its UEs, base+U .. base+P-1 are padding. P = U, or the next power of
+// two where that costs no envs per wavefront (U = 15 -> 16, U = 30 -> 32): then segments are
+// whole DPP rows / row pairs and per-env sums need no cross-row shuffles.
 struct LaneMap {
   int seg, u, base;
   uint64_t segmask, lt;
 };
 
-__device__ __forceinline__ LaneMap lane_map(int lane, int U) {
+__host__ __device__ constexpr int pitch_of(int U) {
+  return (U > 8 && U <= 16 && 64 / 16 == 64 / U) ? 16
+         : (U > 16 && U <= 32 && 64 / 32 == 64 / U) ? 32 : U;
+}
+
+template <int PC>
+__device__ __forceinline__ LaneMap lane_map(int lane, int P) {
   LaneMap m;
-  // lane / U through float: (lane + 0.5) / U is >= 0.5/U away from an integer
-  m.seg = (int)(((float)lane + 0.5f) * (1.0f / (float)U));
-  m.u = lane - m.seg * U;
-  m.base = m.seg * U;
-  m.segmask = (U >= 64) ? ~0ull : (((1ull << U) - 1ull) << m.base);
+  if (PC == 16 || PC == 32) {
+    m.seg = lane / PC;
+  } else {
+    // lane / P through float: (lane + 0.5) / P is >= 0.5/P away from an integer
+    m.seg = (int)(((float)lane + 0.5f) * (1.0f / (float)P));
+  }
+  m.u = lane - m.seg * P;
+  m.base = m.seg * P;
+  m.segmask = (P >= 64) ? ~0ull : (((1ull << P) - 1ull) << m.base);
   m.lt = (1ull << lane) - 1ull;
   return m;
 }
@@ -380,7 +418,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
                                                               const uint8_t* __restrict__ mask) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const LaneMap m = lane_map(lane, kp.U);
+  const LaneMap m = lane_map<0>(lane, kp.U);
   const int e = wave * kp.envs_per_wave + m.seg;
   if (m.seg >= kp.envs_per_wave || e >= kp.E) return;
   if (mask != nullptr && !mask[e]) return;
@@ -417,9 +455,14 @@ template <bool PER_ENV_BS, bool LEAN, int UC>
 __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, const GroupIn& cur, int e,
-                                             bool valid) {
+                                             bool env_ok, int* __restrict__ hist) {
+  constexpr int PC = UC ? pitch_of(UC) : 0;
+  constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   const int U = UC ? UC : kp.U;
+  const int P = PC ? PC : kp.U;
   const int u = m.u;
+  const bool valid = env_ok && u < U;             // a lane holding a UE
+  const bool leader = ROWS ? u == P - 1 : u == 0;  // the lane of the per-env stores
   const uint64_t segmask = m.segmask, lt = m.lt;
   const bool want_metrics = !LEAN && out.metrics != nullptr;
   const bool exact_util = !LEAN && (out.util64 != nullptr || kp.util_direct);
@@ -439,8 +482,10 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   u128 s_fin = s;  // stream state after this lane's last draw
 
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
-  const bool do_reset = valid && t >= kp.t_end;
-  if (__ballot(do_reset)) {
+  const bool reset_env = env_ok && t >= kp.t_end;  // every lane of the env, padding too
+  const bool do_reset = reset_env && valid;
+  if (__ballot(reset_env)) {
+    if (reset_env) t = 0;
     if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc =
           reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
@@ -448,7 +493,6 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       koff = 2 * U;
       wp = make_int2(-1, -1);
-      t = 0;
     }
   }
 
@@ -516,16 +560,29 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     }
   }
 
-  // ---- 3. n_b of the own serving BS: lanes of the segment with the same index, matched
-  //         bit by bit with ballots (no LDS, no atomics) ---------------------------------
+  // ---- 3. n_b of the own serving BS ---------------------------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
-  uint64_t match = mcon;
-  for (int bit = 0; bit < kp.srv_bits; ++bit) {
-    const bool on = (srv >> bit) & 1;
-    const uint64_t mb = __ballot(on);
-    match &= on ? mb : ~mb;
+  int n;
+  if (kp.hist_lds) {
+    // per-env histogram in the wavefront's own LDS slice [G][B]: zero, count, read back
+    // (one wavefront's LDS instructions execute in order: no barrier)
+    int* h = hist + m.seg * kp.B;
+    if (env_ok)
+      for (int k = u; k < kp.B; k += P) h[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (srv >= 0) __hip_atomic_fetch_add(h + srv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_wave_barrier();
+    n = srv >= 0 ? h[srv] : 0;
+  } else {
+    // lanes of the segment with the same index, matched bit by bit with ballots
+    uint64_t match = mcon;
+    for (int bit = 0; bit < kp.srv_bits; ++bit) {
+      const bool on = (srv >> bit) & 1;
+      const uint64_t mb = __ballot(on);
+      match &= on ? mb : ~mb;
+    }
+    n = (int)__popcll(match);
   }
-  const int n = __popcll(match);
 
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
@@ -540,9 +597,10 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
   const uint64_t mact = __ballot(active) & segmask;
   const int nact = __popcll(mact);
-  const double sum_u = seg_sum(util, active, U, u);
+  const double sum_u = ROWS ? seg_sum_rows<PC>(util, active) : seg_sum(util, active, U, u);
   double sum_r = 0.0;
-  if (want_metrics) sum_r = seg_sum(rate, srv >= 0, U, u);
+  if (want_metrics)
+    sum_r = ROWS ? seg_sum_rows<PC>(rate, srv >= 0) : seg_sum(rate, srv >= 0, U, u);
 
   // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
@@ -555,20 +613,20 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
     if (!LEAN && out.util64) out.util64[idx] = active ? util : __builtin_nan("");
-    if (u == 0) {
-      // np.mean; the lean path divides in float32 (the reward output is float32)
-      const double mean_u =
-          LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
-                           : kp.lower)
-               : (nact > 0 ? sum_u / (double)nact : kp.lower);
-      st.t[e] = t + 1;
-      out.reward[e] = (float)mean_u;
-      out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
-      if (want_metrics) {
-        const int ncon = __popcll(mcon);
-        const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
-        out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
-      }
+  }
+  if (env_ok && leader) {
+    // np.mean; the lean path divides in float32 (the reward output is float32)
+    const double mean_u =
+        LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
+                         : kp.lower)
+             : (nact > 0 ? sum_u / (double)nact : kp.lower);
+    st.t[e] = t + 1;
+    out.reward[e] = (float)mean_u;
+    out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
+    if (want_metrics) {
+      const int ncon = __popcll(mcon);
+      const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
+      out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
     }
   }
 }
@@ -591,16 +649,20 @@ __device__ __forceinline__ int block_slot(int remap) {
 template <bool PER_ENV_BS, bool LEAN, int UC>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb, int g0, int ngroups) {
+  extern __shared__ int lds_hist[];  // [waves][G][B] when kp.hist_lds
   const int lane = threadIdx.x & 63;
   const int g = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
+  constexpr int PC = UC ? pitch_of(UC) : 0;
   const int U = UC ? UC : kp.U;
-  const int G = UC ? 64 / (UC ? UC : 1) : kp.envs_per_wave;
-  const LaneMap m = lane_map(lane, U);
+  const int P = PC ? PC : kp.U;
+  const int G = PC ? 64 / (PC ? PC : 1) : kp.envs_per_wave;
+  const LaneMap m = lane_map<PC>(lane, P);
   const int e = g * G + m.seg;
-  const bool valid = (m.seg < G) && (e < kp.E);
-  const GroupIn a = load_group(kp, st, e, m.u, U);
-  packed_group<PER_ENV_BS, LEAN, UC>(kp, st, out, tb, m, a, e, valid);
+  const bool env_ok = (m.seg < G) && (e < kp.E);
+  const GroupIn a = load_group(kp, st, e, min(m.u, U - 1), U);
+  packed_group<PER_ENV_BS, LEAN, UC>(kp, st, out, tb, m, a, e, env_ok,
+                                     lds_hist + (threadIdx.x >> 6) * G * kp.B);
 }
 
 // ------------------------------------------------------------------------------------
@@ -934,6 +996,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.first_step_active = params->first_step_active;
   kp.movement_reseed = params->movement_reseed;
   kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
+  kp.hist_lds = params->num_ues <= 64 && kp.envs_per_wave * params->num_bs <= 1024;
   kp.Wd = (double)params->width;
   kp.Hd = (double)params->height;
   kp.vel = params->velocity;
@@ -1145,12 +1208,14 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !kp.util_direct;
   const StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
+  const size_t shmem =
+      kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;
   // split on a block boundary
   const int half = (groups / 2 + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
   if (c->parts == 1 || half <= 0 || half >= groups) {
     const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     for (int i = 0; i < nsteps; ++i)
-      k<<<dim3(blocks), dim3(kPackedBlock), 0, stream>>>(kp, ks, ko, tb, 0, groups);
+      k<<<dim3(blocks), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, 0, groups);
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }
@@ -1159,8 +1224,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   MEV_HIP(hipEventRecord(c->ev_fork, stream));
   MEV_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   for (int i = 0; i < nsteps; ++i) {
-    k<<<dim3(blocks0), dim3(kPackedBlock), 0, stream>>>(kp, ks, ko, tb, 0, half);
-    k<<<dim3(blocks1), dim3(kPackedBlock), 0, c->aux>>>(kp, ks, ko, tb, half, groups);
+    k<<<dim3(blocks0), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, 0, half);
+    k<<<dim3(blocks1), dim3(kPackedBlock), shmem, c->aux>>>(kp, ks, ko, tb, half, groups);
   }
   MEV_HIP(hipGetLastError());
   MEV_HIP(hipEventRecord(c->ev_join, c->aux));
