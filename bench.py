@@ -79,15 +79,19 @@ def cpu_baseline(budget_s: float, procs: int):
                        f"(no JSON dump): {steps} env-steps in {wall:.1f} s")}
 
 
-def load_traffic(workload: str, envs: int):
+def load_profile(workload: str, envs: int):
+    """(HBM bytes per launch from the PMC passes, rocprofv3 average step-kernel duration in
+    ms) of the committed profile of this workload (tools/profile.sh + tools/pmc_summary.py),
+    or Nones."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
-    ent = d.get(f"{workload}@{envs}")
-    return None if ent is None else ent.get("hbm_bytes_per_launch")
+        return None, None
+    ent = d.get(f"{workload}@{envs}") or {}
+    avg_ns = ent.get("rocprof_kernel_avg_ns")
+    return ent.get("hbm_bytes_per_launch"), (avg_ns * 1e-6 if avg_ns else None)
 
 
 def main():
@@ -98,6 +102,8 @@ def main():
     ap.add_argument("--workload", default="mobile-large-central-v0")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--stream-split", type=int, default=0, choices=(0, 1, 2),
+                    help="mev_params.stream_split (2: two env halves on two HIP streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
@@ -136,7 +142,8 @@ def main():
 
     E = args.envs
     seeds = shard_seeds(1000, E, rank)  # rank r owns global envs [r*E, (r+1)*E)
-    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]))
+    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
+                          stream_split=args.stream_split)
     U, B = env.num_ues, env.num_bs
     per_env_bs = env.engine.bs_per_env
     parts = env.engine.launch_parts
@@ -185,7 +192,7 @@ def main():
         bpe = algorithmic_bytes_per_env_step(U, per_env_bs, B)
         algo_bytes = E * bpe
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.workload, E)
+        traffic, rocprof_ms = load_profile(args.workload, E)
         out = {
             "metric": METRIC,
             "value": value,
@@ -207,6 +214,7 @@ def main():
                          "traffic": traffic,
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "kernel_ms": kern_ms,
+                         "rocprof_kernel_ms": rocprof_ms,
                          "launch_shape": (f"{parts} halves per step on {parts} HIP streams"
                                           if parts > 1 else "one kernel per step")},
             "cpu_baseline": cpu,

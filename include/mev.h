@@ -77,10 +77,10 @@ typedef struct mev_params {
   int32_t movement_reseed;   /* 1: movement RNG re-seeded every episode (movement_params
                                 reset_rng_episode=True, base.py:133, movement.py:16-18);
                                 0: one stream continued across episodes */
-  int32_t stream_split;      /* mev_step launch shape: 0 auto, 1 one kernel per step on the
-                                caller's stream, 2 the env batch in two halves on the caller's
-                                stream and a context-owned stream (joined before return), so
-                                one half's tail overlaps the other half's start */
+  int32_t stream_split;      /* mev_step launch shape: 0 (auto) or 1: one kernel per step on
+                                the caller's stream; 2: the env batch in two halves on the
+                                caller's stream and a context-owned stream (joined before
+                                return), so one half's tail overlaps the other half's start */
   double velocity;        /* UE velocity (base.py:119, custom.py:16-18) */
   double bs_bw, bs_freq, bs_tx, bs_height;        /* base.py:117 */
   double ue_snr_tr, ue_noise, ue_height;          /* base.py:118-123 */

@@ -120,6 +120,7 @@ def main():
             "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
             "fetch_bytes_per_launch_corrected": summary["fetch_bytes_per_launch_corrected"],
             "write_bytes_per_launch": summary["write_bytes_per_launch"],
+            "rocprof_kernel_avg_ns": summary.get("step_kernel_avg_ns"),
             "source": f"profiles/{tag}_pmc.json"}
         with open(tpath, "w") as f:
             json.dump(traffic, f, indent=2)
