@@ -4,28 +4,34 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-__global__ __launch_bounds__(256) void k_pattern(int4* st, uint64_t* pcg, int* t, float4* obs,
+__global__ __launch_bounds__(256) void k_pattern(int2* st, uint64_t* pcg, int* t, float4* obs,
                                                 int* serving, float* reward, uint8_t* done,
                                                 int E, int U) {
+  // the step kernel's layout: int16x4 UE state (8 B), segments of pitch P (32 for U = 30)
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int G = 64 / U;
-  const int seg = lane / U;
-  const int u = lane - seg * U;
+  const int P = U > 16 && U <= 32 ? 32 : (U > 8 && U <= 16 ? 16 : U);
+  const int G = 64 / P;
+  const int seg = lane / P;
+  const int u = lane - seg * P;
   const int e = wave * G + seg;
   if (seg >= G || e >= E) return;
-  const size_t idx = (size_t)e * U + u;
+  const int uc = u < U ? u : U - 1;
+  const size_t idx = (size_t)e * U + uc;
   const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(pcg + 6 * (size_t)e);
   const ulonglong2 a = pr[0], b = pr[1];
   const int tt = t[e];
-  int4 s = st[idx];
+  int2 s = st[idx];
   s.x += 1;
   s.y += (int)(a.x & 1);
-  st[idx] = s;
-  serving[idx] = s.z;
-  obs[idx] = make_float4((float)s.x, (float)s.y, (float)tt, (float)(b.y & 7));
-  if (u == 0) {
+  if (u < U) {
+    st[idx] = s;
+    serving[idx] = s.y;
+    obs[idx] = make_float4((float)s.x, (float)s.y, (float)tt, (float)(b.y & 7));
+  }
+  if (u == U - 1 && tt % 3 == 0)  // the stream moves in about a third of the env-steps
     *reinterpret_cast<ulonglong2*>(pcg + 6 * (size_t)e) = make_ulonglong2(a.x + 1, a.y);
+  if (u == P - 1) {
     t[e] = tt + 1;
     reward[e] = (float)tt;
     done[e] = (uint8_t)(tt > 19);
@@ -47,7 +53,7 @@ extern "C" int mb_pattern(void* st, void* pcg, void* t, void* obs, void* serving
   const int waves = (E + G - 1) / G;
   for (int r = 0; r < reps; ++r)
   hipLaunchKernelGGL(k_pattern, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     (int4*)st, (uint64_t*)pcg, (int*)t, (float4*)obs, (int*)serving,
+                     (int2*)st, (uint64_t*)pcg, (int*)t, (float4*)obs, (int*)serving,
                      (float*)reward, (uint8_t*)done, E, U);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
