@@ -163,61 +163,6 @@ __device__ __forceinline__ u128 pcg_draw_pair_next(u128 s, u128 inc, double w, d
   return s2;
 }
 
-// numpy pairwise-sum order for n <= 128 (numpy/_core/src/umath/loops_utils.h.src),
-// evaluated by lane 0 of a segment over LDS values a[0..n).
-__device__ __forceinline__ double pairwise_small(const double* a, int n) {
-  if (n < 8) {
-    double res = -0.0;
-    for (int i = 0; i < n; ++i) res += a[i];
-    return res;
-  }
-  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3];
-  double r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += a[i];
-  return res;
-}
-
-// numpy pairwise sum for any n: recursive halving to blocks of <= 128 (PW_BLOCKSIZE).
-__device__ double pairwise_any(const double* a, int n) {
-  if (n <= 128) return pairwise_small(a, n);
-  // explicit stack; depth <= log2(1024/128) + 1
-  struct Frame { int lo, n, stage; double left; };
-  Frame st[8];
-  int sp = 0;
-  st[0] = Frame{0, n, 0, 0.0};
-  double ret = 0.0;
-  while (sp >= 0) {
-    Frame& f = st[sp];
-    if (f.n <= 128) {
-      ret = pairwise_small(a + f.lo, f.n);
-      --sp;
-      continue;
-    }
-    int n2 = f.n / 2;
-    n2 -= n2 % 8;
-    if (f.stage == 0) {
-      f.stage = 1;
-      st[sp + 1] = Frame{f.lo, n2, 0, 0.0};
-      ++sp;
-    } else if (f.stage == 1) {
-      f.left = ret;
-      f.stage = 2;
-      st[sp + 1] = Frame{f.lo + n2, f.n - n2, 0, 0.0};
-      ++sp;
-    } else {
-      ret = f.left + ret;
-      --sp;
-    }
-  }
-  return ret;
-}
-
 // Per-UE movement (movement.py:42-62), exact float64 form: the reference computes
 // position + velocity * v / |v| in float64, then np.round (half-to-even) and astype(int).
 __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel) {
@@ -673,8 +618,8 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
                                                     const uint8_t* __restrict__ mask) {
   __shared__ int lds_cnt[kMaxB];
   __shared__ int lds_wtot[3][16];
-  __shared__ double lds_util[kMaxU];
-  __shared__ double lds_rate[kMaxU];
+  __shared__ int2 lds_key[kMaxB + 1];  // the env's station keys (see k_assoc_map / below)
+  __shared__ double lds_sum[2][16];
 
   const int e = blockIdx.x;
   const int u = threadIdx.x;
@@ -737,7 +682,26 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
                       (kp.first_step_active || t != 0);
   const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
-  for (int i = u; i < nb; i += blockDim.x) lds_cnt[i] = 0;
+  // station keys of this env in LDS: {m as int16x2, c = ((|q|^2 + 2^21) << 10) | j}; with
+  // the map <= 512 x 512 and every station in [0, 512)^2, m = -64 q and the key is ONE dot
+  // product with accumulator, dot2(32 p, m) + c = ((|p - q|^2 - |p|^2 + 2^21) << 10) | j;
+  // otherwise m = -2 q and key = (dot2(p, m) << 10) + c. (|p|^2 is common to all stations.)
+  const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+  bool in512 = true;
+  for (int i = u; i < nb; i += blockDim.x) {
+    const int2 q = bsx[i];
+    in512 = in512 && q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
+  }
+  const bool scaled = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512;
+  for (int i = u; i < nb; i += blockDim.x) {
+    lds_cnt[i] = 0;
+    const int2 q = bsx[i];
+    const int f = scaled ? -64 : -2;
+    const s16x2 m2 = {(short)(f * q.x), (short)(f * q.y)};
+    lds_key[i] = make_int2(__builtin_bit_cast(int, m2),
+                           (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) |
+                                 (unsigned)i));
+  }
 
   // ---- 1. movement: workgroup exclusive scan of "needs waypoint" in ue_id order -------
   const bool need = active && wp.x < 0;
@@ -748,12 +712,12 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     lds_wtot[1][w] = __popcll(mact);
   }
   __syncthreads();
-  int pre_need = 0, tot_need = 0, pre_act = 0, tot_act = 0;
+  int pre_need = 0, tot_need = 0, tot_act = 0;
   for (int i = 0; i < nw; ++i) {
-    const int cn = lds_wtot[0][i], ca = lds_wtot[1][i];
-    if (i < w) { pre_need += cn; pre_act += ca; }
+    const int cn = lds_wtot[0][i];
+    if (i < w) pre_need += cn;
     tot_need += cn;
-    tot_act += ca;
+    tot_act += lds_wtot[1][i];
   }
   if (need) {
     u128 su = pcg_advance(s, inc, 2 * (pre_need + __popcll(mneed & lt)), tb.jump);
@@ -762,21 +726,44 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   }
   if (active) move_ue(pos, wp, kp);
 
-  // ---- 2. association (BS coordinates are workgroup-uniform: scalar loads) ------------
+  // ---- 2. association: min over the env's station keys (LDS broadcast reads, two
+  //         stations per 16-byte read) --------------------------------------------------
   unsigned best = UINT_MAX;
   if (active) {
-    const int2* bs = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
-    const s16x2 pu = {(short)pos.x, (short)pos.y};
-#pragma unroll 8
-    for (int b = 0; b < nb; ++b) {
-      const int2 p = bs[b];
-      const s16x2 d = pu - s16x2{(short)p.x, (short)p.y};
-      const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
-      const unsigned key = (d2 << kKeyBits) | (unsigned)b;
-      best = min(best, key);
+    const int4* kk2 = reinterpret_cast<const int4*>(lds_key);
+    const int npair = nb >> 1;
+    if (scaled) {
+      const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
+#pragma unroll 4
+      for (int i = 0; i < npair; ++i) {
+        const int4 k = kk2[i];
+        const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.x), k.y, false);
+        const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.z), k.w, false);
+        best = min(best, min(k0, k1));
+      }
+      if (nb & 1) {
+        const int2 k = lds_key[nb - 1];
+        best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.x), k.y, false));
+      }
+    } else {
+      const s16x2 pu = {(short)pos.x, (short)pos.y};
+#pragma unroll 4
+      for (int i = 0; i < npair; ++i) {
+        const int4 k = kk2[i];
+        const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.x), 0, true);
+        const int d1 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.z), 0, true);
+        best = min(best, min(((unsigned)d0 << kKeyBits) + (unsigned)k.y,
+                             ((unsigned)d1 << kKeyBits) + (unsigned)k.w));
+      }
+      if (nb & 1) {
+        const int2 k = lds_key[nb - 1];
+        const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.x), 0, true);
+        best = min(best, ((unsigned)d0 << kKeyBits) + (unsigned)k.y);
+      }
     }
   }
-  const int d2s = (int)(best >> kKeyBits);
+  // d2 of the best station: e - 2^21 + |p|^2
+  const int d2s = (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
   const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
 
   // ---- 3. per-BS counts via LDS atomics ---------------------------------------------
@@ -784,21 +771,27 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   const uint64_t mcon = __ballot(srv >= 0);
   if (lane == 0) lds_wtot[2][w] = __popcll(mcon);
   __syncthreads();
-  int pre_con = 0, tot_con = 0;
-  for (int i = 0; i < nw; ++i) {
-    const int cc = lds_wtot[2][i];
-    if (i < w) pre_con += cc;
-    tot_con += cc;
-  }
+  int tot_con = 0;
+  for (int i = 0; i < nw; ++i) tot_con += lds_wtot[2][i];
 
   // ---- 4. rate + utility -------------------------------------------------------------
   double cents = 0.0, rate = 0.0;
   if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv]);
   if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
-  if (active) lds_util[pre_act + __popcll(mact & lt)] = util;
   const bool want_metrics = out.metrics != nullptr;
-  if (want_metrics && srv >= 0) lds_rate[pre_con + __popcll(mcon & lt)] = rate;
+  // reward / mean rate: float64 workgroup sums (wavefront xor-tree, then across wavefronts)
+  {
+    double su = active ? util : 0.0, sr = (want_metrics && srv >= 0) ? rate : 0.0;
+    for (int off = 32; off > 0; off >>= 1) {
+      su += __shfl_xor(su, off);
+      if (want_metrics) sr += __shfl_xor(sr, off);
+    }
+    if (lane == 0) {
+      lds_sum[0][w] = su;
+      lds_sum[1][w] = sr;
+    }
+  }
   __syncthreads();
 
   if (valid) {
@@ -810,7 +803,12 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
   }
   if (u == 0) {
-    const double mean_u = tot_act > 0 ? pairwise_any(lds_util, tot_act) / (double)tot_act : kp.lower;
+    double sum_u = 0.0, sum_r = 0.0;
+    for (int i = 0; i < nw; ++i) {
+      sum_u += lds_sum[0][i];
+      sum_r += lds_sum[1][i];
+    }
+    const double mean_u = tot_act > 0 ? sum_u / (double)tot_act : kp.lower;
     const u128 s_next = pcg_advance(s, inc, 2 * tot_need, tb.jump);
     uint64_t* pw = st.pcg + (size_t)6 * e;
     *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
@@ -818,7 +816,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     out.reward[e] = (float)mean_u;
     out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
     if (want_metrics) {
-      const double mean_r = tot_con > 0 ? pairwise_any(lds_rate, tot_con) / (double)tot_con : 0.0;
+      const double mean_r = tot_con > 0 ? sum_r / (double)tot_con : 0.0;
       out.metrics[e] = make_float4((float)tot_con, (float)tot_con, (float)mean_u, (float)mean_r);
     }
   }
