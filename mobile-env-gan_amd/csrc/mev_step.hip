@@ -122,24 +122,9 @@ __device__ __forceinline__ uint64_t pcg_output(u128 s) {
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
 
-// Advance the LCG by k steps using the jump table: s' = a^k s + G(k) inc.
-__device__ __forceinline__ u128 pcg_advance(u128 s, u128 inc, int k, const u128* jump) {
-  if (k == 0) return s;
-  const u128 m = jump[2 * k];
-  const u128 g = jump[2 * k + 1];
-  return m * s + g * inc;
-}
-
-// numpy Generator.uniform(0, span): off + scale * next_double, next_double =
-// (next_uint64 >> 11) * 2^-53 (numpy/random/src/distributions/distributions.c);
-// the reference then truncates with int() (movement.py:45-46,67-68).
-__device__ __forceinline__ int pcg_draw_coord(u128& s, u128 inc, double span) {
-  const u128 mult = mk128(PCG_MULT_LO, PCG_MULT_HI);
-  s = s * mult + inc;  // PCG64 advances, then outputs
-  const double d = (double)(pcg_output(s) >> 11) * (1.0 / 9007199254740992.0);
-  return (int)(0.0 + span * d);
-}
-
+// numpy Generator.uniform(0, span) is off + scale * next_double with next_double =
+// (next_uint64 >> 11) * 2^-53 (numpy/random/src/distributions/distributions.c); the reference
+// then truncates with int() (movement.py:45-46,67-68). PCG64 advances, then outputs.
 // The two draws (x then y) of a waypoint / initial position at stream offsets k+1, k+2:
 // jump straight to offset k+1 with the table, then one step with the constant multiplier.
 // Returns the stream state after both draws.
@@ -268,6 +253,15 @@ __device__ __forceinline__ double seg_sum(double v, bool take, int U, int u) {
   return x;
 }
 
+// Inclusive prefix sum within each 16-lane DPP row (all lanes active).
+__device__ __forceinline__ int row_scan_i32(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  return x;
+}
+
 // float64 DPP move (both halves), invalid source lanes / masked rows read 0.0
 template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -371,19 +365,18 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
   const ulonglong2 pa = pr[0], pb = pr[1], pc = pr[2];
   const u128 inc = mk128(pb.x, pb.y);
   const u128 s0 = kp.movement_reseed ? mk128(pc.x, pc.y) : mk128(pa.x, pa.y);
-  u128 su = pcg_advance(s0, inc, 2 * m.u, tb.jump);
-  const int x = pcg_draw_coord(su, inc, kp.Wd);
-  const int y = pcg_draw_coord(su, inc, kp.Hd);
+  int x, y;
+  const u128 s_fin = pcg_draw_pair(s0, inc, 2 * m.u, tb.jump, kp.Wd, kp.Hd, x, y);
   const size_t idx = (size_t)e * kp.U + m.u;
   store_ue(st.ue_state + idx, make_int2(x, y), make_int2(-1, -1));
   out.serving[idx] = -1;
   out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
   if (out.rate64) out.rate64[idx] = 0.0;
   if (out.util64) out.util64[idx] = 0.0;
-  if (m.u == 0) {
-    const u128 s = pcg_advance(s0, inc, 2 * kp.U, tb.jump);
+  if (m.u == kp.U - 1)  // the state after the env's 2U initial draws
     *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
-        make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+        make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
+  if (m.u == 0) {
     st.t[e] = 0;
     out.reward[e] = 0.f;
     out.done[e] = 0;
@@ -618,7 +611,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
                                                     const uint8_t* __restrict__ mask) {
   __shared__ int lds_cnt[kMaxB];
   __shared__ int lds_wtot[3][16];
-  __shared__ int2 lds_key[kMaxB + 1];  // the env's station keys (see k_assoc_map / below)
+  __shared__ __align__(16) int2 lds_key[kMaxB + 2];  // the env's station keys (below)
   __shared__ double lds_sum[2][16];
 
   const int e = blockIdx.x;
@@ -639,20 +632,18 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   const bool do_reset = RESET ? (mask == nullptr || mask[e]) : (t >= kp.t_end);
   if (RESET && !do_reset) return;  // uniform over the workgroup
 
-  u128 s;
+  // stream bookkeeping as in the packed kernel: draws of this step start at offset koff of
+  // `s`; the lane of the env's last draw writes the new stream state back
+  u128 s = mk128(a.x, a.y), s_fin = s;
+  int koff = 0;
   int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
   if (do_reset) {
     const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
-    const u128 s0 = kp.movement_reseed ? mk128(c.x, c.y) : mk128(a.x, a.y);
-    if (valid) {
-      u128 su = pcg_advance(s0, inc, 2 * u, tb.jump);
-      pos.x = pcg_draw_coord(su, inc, kp.Wd);
-      pos.y = pcg_draw_coord(su, inc, kp.Hd);
-    }
-    s = pcg_advance(s0, inc, 2 * U, tb.jump);
+    if (kp.movement_reseed) s = mk128(c.x, c.y);
+    if (valid) s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+    koff = 2 * U;
     t = 0;
   } else {
-    s = mk128(a.x, a.y);
     if (valid) {
       const int4 sv = load_ue(st.ue_state + idx);
       pos = make_int2(sv.x, sv.y);
@@ -668,9 +659,12 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
       if (out.rate64) out.rate64[idx] = 0.0;
       if (out.util64) out.util64[idx] = 0.0;
     }
-    if (u == 0) {
+    if (u == U - 1) {  // the state after the 2U initial draws
       uint64_t* pw = st.pcg + (size_t)6 * e;
-      *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+      *reinterpret_cast<ulonglong2*>(pw) =
+          make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
+    }
+    if (u == 0) {
       st.t[e] = 0;
       out.reward[e] = 0.f;
       out.done[e] = 0;
@@ -712,18 +706,16 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
     lds_wtot[1][w] = __popcll(mact);
   }
   __syncthreads();
-  int pre_need = 0, tot_need = 0, tot_act = 0;
-  for (int i = 0; i < nw; ++i) {
-    const int cn = lds_wtot[0][i];
-    if (i < w) pre_need += cn;
-    tot_need += cn;
-    tot_act += lds_wtot[1][i];
-  }
-  if (need) {
-    u128 su = pcg_advance(s, inc, 2 * (pre_need + __popcll(mneed & lt)), tb.jump);
-    wp.x = pcg_draw_coord(su, inc, kp.Wd);
-    wp.y = pcg_draw_coord(su, inc, kp.Hd);
-  }
+  // per-wavefront counts -> workgroup prefix / totals: lane i < nw (<= 16, one DPP row)
+  // holds wavefront i's count, a row scan, then wave-uniform reads of single lanes
+  const int scan_need = row_scan_i32(lane < nw ? lds_wtot[0][lane & 15] : 0);
+  const int scan_act = row_scan_i32(lane < nw ? lds_wtot[1][lane & 15] : 0);
+  const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
+  const int tot_need = __builtin_amdgcn_readlane(scan_need, nw - 1);
+  const int tot_act = __builtin_amdgcn_readlane(scan_act, nw - 1);
+  const int rank = pre_need + (int)__popcll(mneed & lt);
+  if (need) s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
+  const bool own_fin = (need && rank == tot_need - 1) || (do_reset && tot_need == 0 && u == U - 1);
   if (active) move_ue(pos, wp, kp);
 
   // ---- 2. association: min over the env's station keys (LDS broadcast reads, two
@@ -771,8 +763,8 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   const uint64_t mcon = __ballot(srv >= 0);
   if (lane == 0) lds_wtot[2][w] = __popcll(mcon);
   __syncthreads();
-  int tot_con = 0;
-  for (int i = 0; i < nw; ++i) tot_con += lds_wtot[2][i];
+  const int tot_con =
+      __builtin_amdgcn_readlane(row_scan_i32(lane < nw ? lds_wtot[2][lane & 15] : 0), nw - 1);
 
   // ---- 4. rate + utility -------------------------------------------------------------
   double cents = 0.0, rate = 0.0;
@@ -801,6 +793,9 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
                                (float)cents * 0.01f, (float)util);
     if (out.rate64) out.rate64[idx] = rate;
     if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
+    if (own_fin)  // the stream moved (draws, or reset): write the new state back
+      *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+          make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
   }
   if (u == 0) {
     double sum_u = 0.0, sum_r = 0.0;
@@ -809,9 +804,6 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
       sum_r += lds_sum[1][i];
     }
     const double mean_u = tot_act > 0 ? sum_u / (double)tot_act : kp.lower;
-    const u128 s_next = pcg_advance(s, inc, 2 * tot_need, tb.jump);
-    uint64_t* pw = st.pcg + (size_t)6 * e;
-    *reinterpret_cast<ulonglong2*>(pw) = make_ulonglong2((uint64_t)s_next, (uint64_t)(s_next >> 64));
     st.t[e] = t + 1;
     out.reward[e] = (float)mean_u;
     out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
