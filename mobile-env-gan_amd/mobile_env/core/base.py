@@ -196,24 +196,36 @@ class MComCore:
         eng = self._ensure_engine()
         eng.step(1)
         users = self._users()
-        xy = eng.ue_xy[0].cpu().tolist()
+        state = eng.ue_state[0].cpu().tolist()
         srv = eng.serving[0].cpu().tolist()
         rate = eng.rate64[0].cpu().tolist()
         util = eng.util64[0].cpu().tolist()
         self._metric_values = tuple(eng.metrics[0].double().cpu().tolist())
-        for ue, (x, y) in zip(users, xy):
-            ue.x, ue.y = int(x), int(y)
         active = set(self.activeUsers)
+        # the reference's value types (they show in save_epoch_data's CSVs): a regular move
+        # yields numpy ints (movement.py:58-60), a snap the popped waypoint's python ints
+        # (movement.py:53-54); a connected UE's rate and the utility of a positive rate are
+        # numpy floats, the rest python floats (base.py:421-435, utilities.py:45-53)
+        for ue, (x, y, wx, _) in zip(users, state):
+            snapped = ue in active and wx < 0
+            ue.x, ue.y = (int(x), int(y)) if snapped else (np.int64(x), np.int64(y))
         stations = self._stations()
         self.bs2ue_connections = defaultdict(set)
         self.bs2ue_dataRates = {}
+        by_station = defaultdict(list)
         for ue, b in zip(users, srv):
             if b >= 0 and ue in active:
-                bs = stations[b]
+                by_station[b].append(ue)
+        for b in sorted(by_station):  # station order, like the reference's dict iteration
+            bs = stations[b]
+            for ue in by_station[b]:
                 self.bs2ue_connections[bs].add(ue)
-                self.bs2ue_dataRates[(bs, ue)] = rate[ue.ue_id]
+                self.bs2ue_dataRates[(bs, ue)] = np.float64(rate[ue.ue_id])
         self.allUserDataRates = self.user_total_datarates(self.bs2ue_dataRates)
-        self.ue_utilities = {ue: util[ue.ue_id] for ue in self.activeUsers}
+        self.ue_utilities = {
+            ue: (np.float64(util[ue.ue_id]) if srv[ue.ue_id] >= 0 and rate[ue.ue_id] > 0.0
+                 else float(util[ue.ue_id]))
+            for ue in self.activeUsers}
 
         if self.dump_root is not None:
             self.save_layout_and_data_rates(epoch_number, curr_step)

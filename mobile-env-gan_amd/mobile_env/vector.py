@@ -56,7 +56,7 @@ def _bs_layouts(spec, num_envs, seeds, device):
 class VectorMobileEnv:
     def __init__(self, env_id: str, num_envs: int = 1, device=None, seed: int = 2024,
                  config: Optional[dict] = None, metrics: bool = False, rate64: bool = False,
-                 stream_split: int = 0):
+                 util64: bool = False, stream_split: int = 0):
         spec = registry.spec(env_id)
         cfg = deep_dict_merge(default_config(), config or {})
         if spec["velocity"] is not None:
@@ -81,7 +81,7 @@ class VectorMobileEnv:
             util_coeffs=tuple(cfg["utility_params"]["coeffs"]),
             stream_split=stream_split)
         self.engine = StepEngine(p, bs_xy, self.seeds.numpy(), bs_count=bs_count, device=device,
-                                 metrics=metrics, rate64=rate64)
+                                 metrics=metrics, rate64=rate64, util64=util64)
         U = self.num_ues
         if self.mode == "central":
             self.single_observation_space = Box(-float("inf"), float("inf"), (U * 4,),
