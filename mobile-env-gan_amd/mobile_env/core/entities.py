@@ -11,8 +11,10 @@ from typing import NamedTuple, Tuple
 
 
 class Point(NamedTuple):
-    x: int
-    y: int
+    """shapely.geometry.Point of the integer-truncated coordinates (entities.py:24-26,52-54):
+    like shapely, the coordinates read back as floats."""
+    x: float
+    y: float
 
     def distance(self, other: "Point") -> float:
         dx, dy = self.x - other.x, self.y - other.y
@@ -31,7 +33,7 @@ class BaseStation:
 
     @property
     def point(self) -> Point:
-        return Point(int(self.x), int(self.y))
+        return Point(float(int(self.x)), float(int(self.y)))
 
     def __str__(self):
         return f"BS: {self.bs_id}"
@@ -51,7 +53,7 @@ class UserEquipment:
 
     @property
     def point(self) -> Point:
-        return Point(int(self.x), int(self.y))
+        return Point(float(int(self.x)), float(int(self.y)))
 
     def __str__(self):
         return f"UE: {self.ue_id}"
