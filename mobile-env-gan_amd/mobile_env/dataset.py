@@ -149,7 +149,8 @@ class DatasetWriter:
     step has been recorded."""
 
     def __init__(self, engine, root: str, envs=None, epoch_of: Optional[Callable] = None,
-                 depth: int = 8, station_positions: bool = True):
+                 depth: int = 8, station_positions: bool = True,
+                 episode_steps: Optional[int] = None):
         import torch
         eng = getattr(engine, "engine", engine)
         if eng.rate64 is None or eng.util64 is None:
@@ -164,6 +165,8 @@ class DatasetWriter:
                                                          enumerate(self.envs)}, _n=self.n:
                                      k * _n + _pos[int(e)])
         self.station_positions = station_positions
+        # the driver's save_epoch_data after this many steps (default: the episode length)
+        self.episode_steps = episode_steps or eng.p.t_end
         self._stream = torch.cuda.Stream(device=eng.device)
         self._free = queue.Queue()
         for _ in range(depth):
@@ -231,7 +234,6 @@ class DatasetWriter:
 
     def _write_step(self, h):
         p = self.eng.p
-        t_end = p.t_end
         for i in range(self.n):
             t = int(h["t"][i])  # time after the step: curr_step = t - 1
             step = t - 1
@@ -255,6 +257,6 @@ class DatasetWriter:
                                            util, active))
             self._hist[i].add(xy, active & (wpx < 0), h["serving"][i], h["rate"][i], util,
                               active)
-            if t >= t_end:
+            if step == self.episode_steps - 1:
                 files.update(self._hist[i].files(epoch))
             write_files(self.root, files)

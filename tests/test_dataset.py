@@ -167,3 +167,26 @@ def test_facade_dump_matches_reference(tmp_path):
             env.save_epoch_data(ep)
         env.close()
         assert_same_files(read_tree(str(root)), run["files"])
+
+
+def test_draw_layouts_follow_the_reference_call_order():
+    from mobile_env.collect import draw_layouts
+    from mobile_env.scenarios.custom import MComCustom
+    random.seed(11)
+    want = [[[bs.x, bs.y] for bs in MComCustom.generate_base_stations(
+        MComCustom.default_config())] for _ in range(5)]
+    xy, cnt = draw_layouts(random.Random(11), 5)
+    assert [xy[k, :cnt[k]].tolist() for k in range(5)] == want
+
+
+@pytest.mark.gpu
+def test_batched_collect_matches_reference_driver(tmp_path):
+    """collect_data (every notebook epoch as one env of a batch) writes the files of the
+    reference's sequential collectData2 driver, for the same random seed."""
+    from mobile_env.collect import collect_data
+    g = golden()
+    for run in g["runs"]:
+        root = tmp_path / f"seed{run['random_seed']}"
+        collect_data(g["epochs"], str(root), random_seed=run["random_seed"], steps=g["steps"],
+                     device="cuda", batch=1 if run["random_seed"] else 64)
+        assert_same_files(read_tree(str(root)), run["files"])
