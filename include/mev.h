@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 3
+#define MEV_ABI_VERSION 4
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -86,6 +86,8 @@ typedef struct mev_params {
   double ue_snr_tr, ue_noise, ue_height;          /* base.py:118-123 */
   double util_lower, util_upper;                  /* base.py:136 */
   double util_w1, util_w2, util_w3;               /* coeffs (10, 0, 10) */
+  double qoe_low;         /* low-QoE threshold of the layout score (chooseBaseStation.ipynb
+                             cell 5: low_qoe_threshold = 0.0) */
 } mev_params;
 
 typedef struct mev_state {
@@ -104,6 +106,10 @@ typedef struct mev_outputs {
   double* rate64;   /* may be NULL */
   double* util64;   /* may be NULL */
   float* metrics;   /* may be NULL */
+  double* qoe_stats; /* may be NULL: [E][4] per-episode statistics of the rounded QoE values
+                        round(u, 2) of the active UEs (the values save_epoch_data writes,
+                        base.py:269): {count, sum, sum of squares, count below qoe_low};
+                        restarted at every episode's first step */
 } mev_outputs;
 
 typedef struct mev_ctx mev_ctx;

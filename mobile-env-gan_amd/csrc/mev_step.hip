@@ -69,6 +69,7 @@ struct KParams {
   float vel_f;
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
+  double qoe_low;
 };
 
 struct KState {
@@ -87,6 +88,7 @@ struct KOut {
   double* rate64;
   double* util64;
   float4* metrics;
+  double4* qoe_stats;  // [E] {count, sum, sum of squares, count below qoe_low}
 };
 
 struct KTables {
@@ -403,7 +405,8 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const bool leader = ROWS ? u == P - 1 : u == 0;  // the lane of the per-env stores
   const uint64_t segmask = m.segmask, lt = m.lt;
   const bool want_metrics = !LEAN && out.metrics != nullptr;
-  const bool exact_util = !LEAN && (out.util64 != nullptr || kp.util_direct);
+  const bool want_qoe = !LEAN && out.qoe_stats != nullptr;
+  const bool exact_util = !LEAN && (out.util64 != nullptr || kp.util_direct || want_qoe);
   const bool want_rate = !LEAN && (out.rate64 != nullptr || want_metrics || exact_util);
   const size_t idx = (size_t)e * U + u;
   int t = cur.t;
@@ -539,6 +542,15 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   double sum_r = 0.0;
   if (want_metrics)
     sum_r = ROWS ? seg_sum_rows<PC>(rate, srv >= 0) : seg_sum(rate, srv >= 0, U, u);
+  // per-episode statistics of the rounded QoE values (numpy round(u, 2) = rint(100 u) / 100)
+  double sum_q = 0.0, sum_q2 = 0.0;
+  int nlow = 0;
+  if (want_qoe) {
+    const double q = rint(util * 100.0) / 100.0;
+    sum_q = ROWS ? seg_sum_rows<PC>(q, active) : seg_sum(q, active, U, u);
+    sum_q2 = ROWS ? seg_sum_rows<PC>(q * q, active) : seg_sum(q * q, active, U, u);
+    nlow = (int)__popcll(__ballot(active && q < kp.qoe_low) & segmask);
+  }
 
   // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
@@ -565,6 +577,14 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       const int ncon = __popcll(mcon);
       const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
       out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
+    }
+    if (want_qoe) {
+      double4 a = t == 0 ? make_double4(0.0, 0.0, 0.0, 0.0) : out.qoe_stats[e];
+      a.x += (double)nact;
+      a.y += sum_q;
+      a.z += sum_q2;
+      a.w += (double)nlow;
+      out.qoe_stats[e] = a;
     }
   }
 }
@@ -612,7 +632,7 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   __shared__ int lds_cnt[kMaxB];
   __shared__ int lds_wtot[3][16];
   __shared__ __align__(16) int2 lds_key[kMaxB + 2];  // the env's station keys (below)
-  __shared__ double lds_sum[2][16];
+  __shared__ double lds_sum[4][16];
 
   const int e = blockIdx.x;
   const int u = threadIdx.x;
@@ -772,18 +792,30 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
   if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
   const bool want_metrics = out.metrics != nullptr;
-  // reward / mean rate: float64 workgroup sums (wavefront xor-tree, then across wavefronts)
+  const bool want_qoe = out.qoe_stats != nullptr;
+  const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
+  // reward / mean rate / QoE statistics: float64 workgroup sums (wavefront xor-tree, then
+  // across wavefronts)
   {
     double su = active ? util : 0.0, sr = (want_metrics && srv >= 0) ? rate : 0.0;
+    double sq = (want_qoe && active) ? q : 0.0, sq2 = sq * sq;
     for (int off = 32; off > 0; off >>= 1) {
       su += __shfl_xor(su, off);
       if (want_metrics) sr += __shfl_xor(sr, off);
+      if (want_qoe) {
+        sq += __shfl_xor(sq, off);
+        sq2 += __shfl_xor(sq2, off);
+      }
     }
     if (lane == 0) {
       lds_sum[0][w] = su;
       lds_sum[1][w] = sr;
+      lds_sum[2][w] = sq;
+      lds_sum[3][w] = sq2;
     }
   }
+  const uint64_t mlow = __ballot(want_qoe && active && q < kp.qoe_low);
+  if (lane == 0) lds_wtot[0][w] = __popcll(mlow);  // the need counts were read above
   __syncthreads();
 
   if (valid) {
@@ -798,10 +830,22 @@ __global__ __launch_bounds__(1024) void k_step_block(KParams kp, KState st, KOut
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
   }
   if (u == 0) {
-    double sum_u = 0.0, sum_r = 0.0;
+    double sum_u = 0.0, sum_r = 0.0, sum_q = 0.0, sum_q2 = 0.0;
+    int nlow = 0;
     for (int i = 0; i < nw; ++i) {
       sum_u += lds_sum[0][i];
       sum_r += lds_sum[1][i];
+      sum_q += lds_sum[2][i];
+      sum_q2 += lds_sum[3][i];
+      nlow += lds_wtot[0][i];
+    }
+    if (want_qoe) {
+      double4 a = t == 0 ? make_double4(0.0, 0.0, 0.0, 0.0) : out.qoe_stats[e];
+      a.x += (double)tot_act;
+      a.y += sum_q;
+      a.z += sum_q2;
+      a.w += (double)nlow;
+      out.qoe_stats[e] = a;
     }
     const double mean_u = tot_act > 0 ? sum_u / (double)tot_act : kp.lower;
     st.t[e] = t + 1;
@@ -991,6 +1035,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.Hd = (double)params->height;
   kp.vel = params->velocity;
   kp.lower = params->util_lower;
+  kp.qoe_low = params->qoe_low;
   kp.upper = params->util_upper;
   kp.w1 = params->util_w1;
   kp.w2 = params->util_w2;
@@ -1168,6 +1213,7 @@ static void to_kernel(const mev_state* st, const mev_outputs* out, KState& ks, K
   ko.rate64 = out->rate64;
   ko.util64 = out->util64;
   ko.metrics = reinterpret_cast<float4*>(out->metrics);
+  ko.qoe_stats = reinterpret_cast<double4*>(out->qoe_stats);
 }
 
 typedef void (*StepKernel)(KParams, KState, KOut, KTables, int, int);
@@ -1194,7 +1240,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                                const KTables& tb, int nsteps, hipStream_t stream) {
   const KParams& kp = c->kp;
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
-  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !kp.util_direct;
+  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
   const StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
   const size_t shmem =
       kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -40,6 +40,7 @@ class MevParams(C.Structure):
         ("ue_snr_tr", C.c_double), ("ue_noise", C.c_double), ("ue_height", C.c_double),
         ("util_lower", C.c_double), ("util_upper", C.c_double),
         ("util_w1", C.c_double), ("util_w2", C.c_double), ("util_w3", C.c_double),
+        ("qoe_low", C.c_double),
     ]
 
 
@@ -51,7 +52,7 @@ class MevState(C.Structure):
 class MevOutputs(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("serving", C.c_void_p), ("reward", C.c_void_p),
                 ("done", C.c_void_p), ("rate64", C.c_void_p), ("util64", C.c_void_p),
-                ("metrics", C.c_void_p)]
+                ("metrics", C.c_void_p), ("qoe_stats", C.c_void_p)]
 
 
 class MevError(RuntimeError):

@@ -19,7 +19,9 @@ tensor                 reference state                      reference file:line
 
 Outputs per step: ``obs [E,U,4] f32`` = (x/W, y/H, data rate, scaled utility),
 ``serving [E,U] i32``, ``reward [E] f32`` (mean utility, metrics.py:25-28), ``done [E] u8``,
-and optionally ``rate64``/``util64 [E,U] f64`` and ``metrics [E,4] f32``.
+and optionally ``rate64``/``util64 [E,U] f64``, ``metrics [E,4] f32`` and ``qoe_stats [E,4] f64``
+(per-episode {count, sum, sum of squares, count below qoe_low} of the rounded QoE values, the
+input of the layout score, mobile_env.scoring).
 """
 from __future__ import annotations
 
@@ -51,6 +53,7 @@ class EngineParams:
     util_upper: float = 20.0
     util_coeffs: tuple = (10.0, 0.0, 10.0)
     stream_split: int = 0  # mev_params.stream_split: 0 auto, 1 single stream, 2 two halves
+    qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
 
     def to_c(self, bs_per_env: bool) -> N.MevParams:
         return N.MevParams(
@@ -67,7 +70,7 @@ class EngineParams:
             ue_height=float(self.ue["height"]),
             util_lower=float(self.util_lower), util_upper=float(self.util_upper),
             util_w1=float(self.util_coeffs[0]), util_w2=float(self.util_coeffs[1]),
-            util_w3=float(self.util_coeffs[2]))
+            util_w3=float(self.util_coeffs[2]), qoe_low=float(self.qoe_low))
 
     @property
     def t_end(self) -> int:
@@ -94,7 +97,8 @@ class StepEngine:
     base.py:156-168); ``bs_xy`` is [B,2] (shared layout) or [E,B,2] (+ ``bs_count`` [E])."""
 
     def __init__(self, params: EngineParams, bs_xy, seeds, bs_count=None, device=None,
-                 rate64: bool = False, util64: bool = False, metrics: bool = False):
+                 rate64: bool = False, util64: bool = False, metrics: bool = False,
+                 qoe_stats: bool = False):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
@@ -138,6 +142,8 @@ class StepEngine:
             self.rate64 = torch.zeros((E, U), dtype=torch.float64, **kw) if rate64 else None
             self.util64 = torch.zeros((E, U), dtype=torch.float64, **kw) if util64 else None
             self.metrics = torch.zeros((E, 4), dtype=torch.float32, **kw) if metrics else None
+            self.qoe_stats = (torch.zeros((E, 4), dtype=torch.float64, **kw) if qoe_stats
+                              else None)
         self.seed(seeds)
         self._bind()
         with torch.cuda.device(device):
@@ -150,7 +156,7 @@ class StepEngine:
                               _ptr(self.bs_xy), _ptr(self.bs_count))
         self._out = N.MevOutputs(_ptr(self.obs), _ptr(self.serving), _ptr(self.reward),
                                  _ptr(self.done), _ptr(self.rate64), _ptr(self.util64),
-                                 _ptr(self.metrics))
+                                 _ptr(self.metrics), _ptr(self.qoe_stats))
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

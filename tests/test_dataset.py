@@ -190,3 +190,50 @@ def test_batched_collect_matches_reference_driver(tmp_path):
         collect_data(g["epochs"], str(root), random_seed=run["random_seed"], steps=g["steps"],
                      device="cuda", batch=1 if run["random_seed"] else 64)
         assert_same_files(read_tree(str(root)), run["files"])
+
+
+def _golden_qoe(files, epoch):
+    """{ue_id: [qoe, ...]} of a golden user_qoe_{epoch}.csv (the notebook eval()s the cells;
+    here the numbers are parsed)."""
+    import re
+    text = files[f"collectData2/UserQoE/user_qoe_{epoch}.csv"]
+    out = {}
+    for line in text.strip().split("\n")[1:]:
+        uid, cell = line.split(",", 1)
+        out[int(uid)] = [float(v) for v in re.findall(r"-?\d+\.\d+(?:e-?\d+)?", cell)]
+    return out
+
+
+def test_layout_scores_formula_matches_notebook():
+    from mobile_env.scoring import layout_scores, qoe_value_reference
+    g = golden()
+    for run in g["runs"]:
+        for ep in range(g["epochs"]):
+            q = _golden_qoe(run["files"], ep)
+            allq = np.hstack(list(q.values()))
+            stats = np.array([[len(allq), allq.sum(), (allq * allq).sum(),
+                               (allq < 0.0).sum()]], dtype=np.float64)
+            got = layout_scores(stats)
+            want = qoe_value_reference(q)
+            for k in want:
+                np.testing.assert_allclose(got[k][0], want[k], rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_gpu_layout_scores_match_notebook_on_reference_files():
+    """qoe_stats accumulated by the step kernel score the reference's epochs like
+    chooseBaseStation.ipynb does from the reference's CSV files."""
+    from mobile_env.scoring import qoe_value_reference, score_layouts
+    g = golden()
+    lays = [layout(r["files"], ep) for r in g["runs"] for ep in range(g["epochs"])]
+    want = [qoe_value_reference(_golden_qoe(r["files"], ep))
+            for r in g["runs"] for ep in range(g["epochs"])]
+    xy = np.zeros((len(lays), 10, 2), dtype=np.int32)
+    cnt = np.array([len(l) for l in lays], dtype=np.int32)
+    for i, l in enumerate(lays):
+        xy[i, :len(l)] = l
+    got = score_layouts(xy, cnt, device="cuda")
+    for i, w in enumerate(want):
+        for k in w:
+            np.testing.assert_allclose(got[k][i], w[k], rtol=1e-12, atol=1e-14, err_msg=k)
+    assert got["best"] == int(np.argmax([w["Score"] for w in want]))
