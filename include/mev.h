@@ -141,6 +141,9 @@ int mev_copy_rate_table(const mev_ctx* ctx, double* dst, int64_t n);
  * Writes n rows of {state_lo, state_hi, inc_lo, inc_hi, state0_lo, state0_hi}
  * (host memory) for non-negative seeds[i] < 2^63. */
 int mev_seed_pcg64(const uint64_t* seeds, int64_t n, uint64_t* pcg_rows);
+/* The same rows computed on the device: seeds and rows are DEVICE pointers, stream-ordered;
+ * a seed >= 2^63 yields an all-zero row (inc = 0) instead of an error. */
+int mev_seed_pcg64_device(const uint64_t* seeds, int64_t n, uint64_t* rows, void* stream);
 
 /* Reset envs: MComCore.reset + MComCustom.reset bookkeeping (base.py:172-209,
  * custom.py:53-54) -- re-seed the movement stream, draw initial positions

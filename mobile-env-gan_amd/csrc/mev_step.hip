@@ -1341,7 +1341,7 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
 // numpy-compatible seeding (host): SeedSequence(seed).generate_state(4, uint64) ->
 // PCG64 srandom (numpy/random/bit_generator.pyx, numpy/random/src/pcg64/pcg64.c).
 // --------------------------------------------------------------------------------------
-static uint32_t ss_hashmix(uint32_t value, uint32_t* hash_const) {
+__host__ __device__ static uint32_t ss_hashmix(uint32_t value, uint32_t* hash_const) {
   value ^= *hash_const;
   *hash_const *= 0x931e8875u;  // MULT_A
   value *= *hash_const;
@@ -1349,13 +1349,13 @@ static uint32_t ss_hashmix(uint32_t value, uint32_t* hash_const) {
   return value;
 }
 
-static uint32_t ss_mix(uint32_t x, uint32_t y) {
+__host__ __device__ static uint32_t ss_mix(uint32_t x, uint32_t y) {
   uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;  // MIX_MULT_L, MIX_MULT_R
   r ^= r >> 16;
   return r;
 }
 
-static void seed_sequence_state(uint64_t seed, uint64_t out_words[4]) {
+__host__ __device__ static void seed_sequence_state(uint64_t seed, uint64_t out_words[4]) {
   uint32_t entropy[2];
   int n_ent = 0;
   uint64_t v = seed;
@@ -1384,29 +1384,55 @@ static void seed_sequence_state(uint64_t seed, uint64_t out_words[4]) {
   for (int i = 0; i < 4; ++i) out_words[i] = (uint64_t)st32[2 * i] | ((uint64_t)st32[2 * i + 1] << 32);
 }
 
+// One pcg row {state, inc, state0} of PCG64(SeedSequence(seed)): pcg64_set_seed with
+// initstate = (w0 << 64) | w1, initseq = (w2 << 64) | w3.
+__host__ __device__ static void seed_row(uint64_t seed, uint64_t* r) {
+  const u128 mult = ((u128)PCG_MULT_HI << 64) | PCG_MULT_LO;
+  uint64_t w[4];
+  seed_sequence_state(seed, w);
+  const u128 initstate = ((u128)w[0] << 64) | w[1];
+  const u128 initseq = ((u128)w[2] << 64) | w[3];
+  const u128 inc = (initseq << 1) | 1;
+  u128 s = 0;
+  s = s * mult + inc;
+  s += initstate;
+  s = s * mult + inc;
+  r[0] = (uint64_t)s;
+  r[1] = (uint64_t)(s >> 64);
+  r[2] = (uint64_t)inc;
+  r[3] = (uint64_t)(inc >> 64);
+  r[4] = r[0];
+  r[5] = r[1];
+}
+
 int mev_seed_pcg64(const uint64_t* seeds, int64_t n, uint64_t* rows) {
   if ((!seeds || !rows) && n > 0) return MEV_EINVAL;
-  const u128 mult = ((u128)PCG_MULT_HI << 64) | PCG_MULT_LO;
   for (int64_t i = 0; i < n; ++i) {
     if (seeds[i] >> 63) return MEV_EINVAL;
-    uint64_t w[4];
-    seed_sequence_state(seeds[i], w);
-    // pcg64_set_seed: initstate = (w0 << 64) | w1, initseq = (w2 << 64) | w3
-    const u128 initstate = ((u128)w[0] << 64) | w[1];
-    const u128 initseq = ((u128)w[2] << 64) | w[3];
-    const u128 inc = (initseq << 1) | 1;
-    u128 s = 0;
-    s = s * mult + inc;
-    s += initstate;
-    s = s * mult + inc;
-    uint64_t* r = rows + 6 * i;
-    r[0] = (uint64_t)s;
-    r[1] = (uint64_t)(s >> 64);
-    r[2] = (uint64_t)inc;
-    r[3] = (uint64_t)(inc >> 64);
-    r[4] = r[0];
-    r[5] = r[1];
+    seed_row(seeds[i], rows + 6 * i);
   }
+  return MEV_OK;
+}
+
+// Device SeedSequence -> PCG64 rows, one thread per env (batched init of large batches).
+__global__ void k_seed_pcg64(const uint64_t* __restrict__ seeds, int64_t n, uint64_t* rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t sd = seeds[i];
+  uint64_t* r = rows + 6 * i;
+  if (sd >> 63) {  // not a valid numpy seed here: an all-zero row (inc = 0 marks it)
+    for (int k = 0; k < 6; ++k) r[k] = 0;
+    return;
+  }
+  seed_row(sd, r);
+}
+
+int mev_seed_pcg64_device(const uint64_t* seeds, int64_t n, uint64_t* rows, void* stream) {
+  if (n < 0 || ((!seeds || !rows) && n > 0)) return MEV_EINVAL;
+  if (n == 0) return MEV_OK;
+  hipLaunchKernelGGL(k_seed_pcg64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, seeds, n, rows);
+  MEV_HIP(hipGetLastError());
   return MEV_OK;
 }
 

@@ -23,7 +23,8 @@ MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
 EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts",
-           "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_update_stations",
+           "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
+           "mev_update_stations",
            "mev_reset", "mev_step", "mev_strerror", "mev_last_hip_error")
 
 
@@ -94,6 +95,8 @@ def lib():
         L.mev_copy_rate_table.restype = C.c_int
         L.mev_seed_pcg64.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
         L.mev_seed_pcg64.restype = C.c_int
+        L.mev_seed_pcg64_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+        L.mev_seed_pcg64_device.restype = C.c_int
         L.mev_update_stations.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mev_update_stations.restype = C.c_int
         L.mev_reset.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),

@@ -197,8 +197,17 @@ class StepEngine:
             s = s[0] + np.arange(self.p.num_envs, dtype=np.int64)
         if len(s) != self.p.num_envs:
             raise ValueError(f"need {self.p.num_envs} seeds, got {len(s)}")
-        rows = N.seed_pcg64((s + 4).astype(np.uint64))
-        self.pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
+        if (s < 0).any() or (s > np.iinfo(np.int64).max - 4).any():
+            raise ValueError("seeds must lie in [0, 2^63 - 5]")
+        if len(s) >= 4096:  # SeedSequence hashing on the device for large batches
+            d_seeds = torch.from_numpy(s + 4).to(self.device)
+            with torch.cuda.device(self.device):
+                N.check(self._lib.mev_seed_pcg64_device(_ptr(d_seeds), len(s), _ptr(self.pcg),
+                                                        self._stream()),
+                        "mev_seed_pcg64_device")
+        else:
+            rows = N.seed_pcg64((s + 4).astype(np.uint64))
+            self.pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
         self.t.fill_(self.p.t_end)
 
     def set_bs_layout(self, bs_xy, bs_count=None):

@@ -95,3 +95,23 @@ def test_make_reset_step_matches_oracle(env_id):
         np.testing.assert_array_equal(trunc.cpu().numpy(), o["done"])
         assert not term.any()
     env.close()
+
+
+def test_device_seeding_equals_host_seeding():
+    """mev_seed_pcg64_device (SeedSequence hashing on the device) == the host version."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from mobile_env.core import _native as N
+    rng = np.random.default_rng(3)
+    seeds = np.concatenate([[0, 1, 4, 2**32 - 1, 2**32, 2**62 + 5, 2**63 - 1],
+                            rng.integers(0, 2**63 - 1, size=5000, dtype=np.int64)]).astype(np.uint64)
+    want = N.seed_pcg64(seeds)
+    d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()
+    rows = torch.zeros((len(seeds), 6), dtype=torch.int64, device="cuda")
+    N.check(N.lib().mev_seed_pcg64_device(C.c_void_p(d_seeds.data_ptr()), len(seeds),
+                                          C.c_void_p(rows.data_ptr()), None), "seed")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rows.cpu().numpy().view(np.uint64), want)
+    st = np.random.PCG64(int(seeds[100])).state["state"]
+    assert int(want[100, 0]) | (int(want[100, 1]) << 64) == st["state"]
