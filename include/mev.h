@@ -64,7 +64,7 @@ extern "C" {
  * "bs" -> bs_*, "ue" -> ue_*, "utility_params" -> util_*, "arrival_params" ep_time ->
  * arrival_exit, EP_MAX_TIME -> ep_max_time, "movement_params" width/height. */
 typedef struct mev_params {
-  int32_t num_envs;       /* E */
+  int32_t num_envs;       /* E; E * U < 2^28 per context (shard larger batches) */
   int32_t num_ues;        /* U, 1..1024 */
   int32_t num_bs;         /* B (max per env), 1..1024 */
   int32_t width, height;  /* map size (base.py:104) */

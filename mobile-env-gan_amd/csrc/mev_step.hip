@@ -98,6 +98,14 @@ struct KTables {
   const int4* assoc;        // [H][W] shared layout: {serving BS or -1, d2, full rate (f64)}
 };
 
+// Element at a 32-bit byte offset from a wave-uniform base: addresses become
+// `global_load v, v_off, s_base` (no 64-bit address arithmetic per lane). The packed kernel
+// uses it for every per-env / per-UE access; mev_create bounds the buffers below 4 GiB.
+template <class T>
+__device__ __forceinline__ T& at(T* base, uint32_t byte_off) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off);
+}
+
 // UE state row {x, y, wx, wy} packed as int16x4: one 8-byte load / store per UE.
 __device__ __forceinline__ int4 load_ue(const int2* p) {
   const int2 v = *p;
@@ -343,11 +351,12 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
                                               int U) {
   const int ec = min(e, kp.E - 1);
   GroupIn g;
-  g.t = st.t[ec];
-  g.s = load_ue(st.ue_state + (size_t)ec * U + u);
-  const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * ec);
-  g.pa = pr[0];
-  g.pb = pr[1];
+  const uint32_t ue = (uint32_t)(ec * U + u);
+  g.t = at(st.t, 4u * (uint32_t)ec);
+  g.s = load_ue(&at(st.ue_state, 8u * ue));
+  ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+  g.pa = at(pr, 48u * (uint32_t)ec);
+  g.pb = at(pr, 48u * (uint32_t)ec + 16u);
   return g;
 }
 
@@ -428,8 +437,7 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   if (__ballot(reset_env)) {
     if (reset_env) t = 0;
     if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
-      const ulonglong2 pc =
-          reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
+      const ulonglong2 pc = at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e + 32u);
       if (kp.movement_reseed) s = mk128(pc.x, pc.y);
       s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       koff = 2 * U;
@@ -494,7 +502,7 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
     // serving station (or -1) and the full rate of that pair -- one 16-byte gather from an
     // L2-resident table replaces the per-station loop and the rate-table read
     const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
-    const int4 r = tb.assoc[yi * kp.W + xi];
+    const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));
     if (active) {
       srv = r.x;
       full = __hiloint2double(r.w, r.z);
@@ -554,12 +562,13 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
 
   // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
-    store_ue(st.ue_state + idx, pos, wp);
-    out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
-                               (float)cents * 0.01f, (float)util);
+    const uint32_t ui = (uint32_t)idx;
+    store_ue(&at(st.ue_state, 8u * ui), pos, wp);
+    at(out.serving, 4u * ui) = srv;
+    at(out.obs, 16u * ui) = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
+                                        (float)cents * 0.01f, (float)util);
     if (own_fin)  // the stream moved (draws, or reset): write the new state back
-      *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+      at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) =
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
     if (!LEAN && out.util64) out.util64[idx] = active ? util : __builtin_nan("");
@@ -570,9 +579,9 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
         LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
                          : kp.lower)
              : (nact > 0 ? sum_u / (double)nact : kp.lower);
-    st.t[e] = t + 1;
-    out.reward[e] = (float)mean_u;
-    out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
+    at(st.t, 4u * (uint32_t)e) = t + 1;
+    at(out.reward, 4u * (uint32_t)e) = (float)mean_u;
+    at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
     if (want_metrics) {
       const int ncon = __popcll(mcon);
       const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
@@ -1002,6 +1011,8 @@ static int validate(const mev_params* p) {
   if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
   if (p->ep_max_time < 1 || p->arrival_exit < 1) return MEV_EINVAL;
   if (p->stream_split < 0 || p->stream_split > 2) return MEV_EINVAL;
+  // every per-UE buffer below 4 GiB (32-bit byte offsets in the step kernel): E U < 2^28
+  if ((int64_t)p->num_envs * p->num_ues >= ((int64_t)1 << 28)) return MEV_EINVAL;
   if (!(p->velocity >= 0.0) || !(p->ue_noise > 0.0) || !(p->util_upper > p->util_lower))
     return MEV_EINVAL;
   return MEV_OK;
