@@ -10,24 +10,26 @@ OUT = os.path.join(ROOT, "mobile-env-gan_amd", "lib")
 
 EDITS = {
     "no_draw": [("  if (mneed_w) {", "  if (false) {")],
-    "no_assoc": [("    const int nb = kp.B;\n    const int2* __restrict__ keys",
-                  "    best = (unsigned)(pos.x & 1023) << kKeyBits;\n    const int nb = 0;\n    const int2* __restrict__ keys")],
-    "no_pairwise": [("  const double sum_u = seg_sum(util, active, U, u);",
+    "no_assoc": [("    const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));",
+                  "    const int4 r = make_int4(xi % 13, yi, xi, yi);")],
+    "no_pairwise": [("  const double sum_u = ROWS ? seg_sum_rows<PC>(util, active) : seg_sum(util, active, U, u);",
                      "  const double sum_u = util;")],
     "no_move": [("  if (active) move_ue(pos, wp, kp);\n\n  // ---- 2.", "\n  // ---- 2.")],
-    "no_match": [("  for (int bit = 0; bit < kp.srv_bits; ++bit) {", "  for (int bit = 0; bit < 0; ++bit) {")],
+    "no_match": [("    n = srv >= 0 ? h[srv] : 0;", "    n = srv >= 0 ? 1 + (srv & 3) : 0;")],
     "no_rate": [("  if (srv >= 0) cents = share_cents(full, n);",
-                 "  if (srv >= 0) cents = (double)(d2s * n);")],
+                 "  if (srv >= 0) cents = (double)((int)full * n);")],
     "no_util": [("    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32(cents, kp);",
                  "    util = cents * 1e-3;")],
 }
 COMPUTE_ONLY = [
-    ("  g.t = st.t[ec];\n  g.s = st.ue_state[(size_t)ec * U + u];",
-     "  g.t = (ec * 7) % 20;\n  g.s = make_int4((ec * 13 + u * 7) % 200, (ec * 3 + u * 11) % 200, (ec + u) % 200, (ec * 5 + u) % 200);"),
-    ("  g.pa = pr[0];\n  g.pb = pr[1];",
-     "  g.pa = make_ulonglong2((uint64_t)pr, 7);\n  g.pb = make_ulonglong2(2 * e + 1, 3);"),
+    ("  g.t = at(st.t, 4u * (uint32_t)ec);\n  g.s = load_ue(&at(st.ue_state, 8u * ue));",
+     "  g.t = (ec * 7) % 20;\n  g.s = make_int4((ec * 13 + u * 7) % 200, (ec * 3 + u * 11) % 200, "
+     "((ec * 7 + u * 13) % 70 == 0) ? -1 : (ec + u * 5) % 200, (ec * 5 + u) % 200);"),
+    ("  g.pa = at(pr, 48u * (uint32_t)ec);\n  g.pb = at(pr, 48u * (uint32_t)ec + 16u);",
+     "  g.pa = make_ulonglong2((uint64_t)pr + ec, 7);\n  g.pb = make_ulonglong2(2 * ec + 1, 3);"),
     ("  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid) {",
      "  // ---- 6. stores ----------------------------------------------------------------------\n  if (valid && kp.E < 0) {"),
+    ("  if (env_ok && leader) {\n    // np.mean;", "  if (env_ok && leader && kp.E < 0) {\n    // np.mean;"),
 ]
 
 
