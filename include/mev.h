@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 4
+#define MEV_ABI_VERSION 5
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -77,6 +77,10 @@ typedef struct mev_params {
   int32_t movement_reseed;   /* 1: movement RNG re-seeded every episode (movement_params
                                 reset_rng_episode=True, base.py:133, movement.py:16-18);
                                 0: one stream continued across episodes */
+  int32_t draw_table;        /* episode draw table (U <= 64, movement_reseed = 1): pairs per
+                                env precomputed from state0 by mev_reset / mev_prepare_draws
+                                (every episode of an env draws the same sequence); -1 auto
+                                (4U + 16), 0 off */
   int32_t stream_split;      /* mev_step launch shape: 0 (auto) or 1: one kernel per step on
                                 the caller's stream; 2: the env batch in two halves on the
                                 caller's stream and a context-owned stream (joined before
@@ -151,6 +155,10 @@ int mev_seed_pcg64_device(const uint64_t* seeds, int64_t n, uint64_t* rows, void
  * Writes obs (positions, rate 0, utility 0), serving = -1. */
 int mev_reset(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
               const uint8_t* env_mask, void* stream);
+/* Rebuild the episode draw tables of the envs with env_mask[e] (all if NULL) from their
+ * pcg rows' state0 (mev_reset does it; call it after changing pcg rows without a reset). */
+int mev_prepare_draws(const mev_ctx* ctx, const mev_state* state, const uint8_t* env_mask,
+                      void* stream);
 
 /* Shared station layout (bs_per_env = 0): (re)derive the association keys the step kernel
  * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the

@@ -61,6 +61,7 @@ struct KParams {
   int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
   int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
   int hist_lds;       // packed shape: per-env BS counts in an LDS histogram ([G][B] per wave)
+  int tab_m;          // episode draw table: pairs per env (0: off)
   float inv_w, inv_h; // obs normalisation
   int d2snap;         // largest integer d2 with sqrt(d2) <= velocity (arrival test)
   float move_band;    // tie band of the float32 movement fast path
@@ -96,6 +97,12 @@ struct KTables {
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
   const double* util;       // [util_kmax + 1]: scaled utility of rate k/100
   const int4* assoc;        // [H][W] shared layout: {serving BS or -1, d2, full rate (f64)}
+  // episode draw table (movement re-seeded every episode => each env's draws of an episode
+  // are a fixed sequence): pair k = the (x, y) of draws 2k, 2k+1 from state0 and the stream
+  // state after them; `drawn` = pairs of the current episode consumed so far
+  const int* tab_xy;        // [E][M] int16x2
+  const u128* tab_st;       // [E][M]
+  int* drawn;               // [E]
 };
 
 // Element at a 32-bit byte offset from a wave-uniform base: addresses become
@@ -343,20 +350,27 @@ __device__ __forceinline__ LaneMap lane_map(int lane, int P) {
 // valid env): a guarded load would make the compiler wait for it at the merge point.
 struct GroupIn {
   int t;
+  int drawn;           // draw-table mode: pairs of the episode consumed so far
   int4 s;              // {x, y, wx, wy}
   ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
 };
 
-__device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st, int e, int u,
-                                              int U) {
+__device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st,
+                                              const KTables& tb, int e, int u, int U) {
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue(&at(st.ue_state, 8u * ue));
-  ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-  g.pa = at(pr, 48u * (uint32_t)ec);
-  g.pb = at(pr, 48u * (uint32_t)ec + 16u);
+  if (kp.tab_m) {  // the stream state is read only when a draw falls beyond the table
+    g.drawn = at(tb.drawn, 4u * (uint32_t)ec);
+    g.pa = g.pb = make_ulonglong2(0, 0);
+  } else {
+    ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+    g.drawn = 0;
+    g.pa = at(pr, 48u * (uint32_t)ec);
+    g.pb = at(pr, 48u * (uint32_t)ec + 16u);
+  }
   return g;
 }
 
@@ -388,6 +402,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
     *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
         make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
   if (m.u == 0) {
+    if (kp.tab_m) tb.drawn[e] = kp.U;  // the U initial pairs of the episode
     st.t[e] = 0;
     out.reward[e] = 0.f;
     out.done[e] = 0;
@@ -421,8 +436,10 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   int t = cur.t;
   int2 pos = make_int2(cur.s.x, cur.s.y);
   int2 wp = make_int2(cur.s.z, cur.s.w);
-  const u128 inc = mk128(cur.pb.x, cur.pb.y);
+  u128 inc = mk128(cur.pb.x, cur.pb.y);
   u128 s = mk128(cur.pa.x, cur.pa.y);
+  const int M = kp.tab_m;  // wave-uniform
+  int drawn = cur.drawn;
 
   // Stream bookkeeping without cross-lane moves: the step's waypoint draws start at offset
   // koff of stream state `s` (koff = 2U right after a reset: the initial positions took the
@@ -436,7 +453,16 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const bool do_reset = reset_env && valid;
   if (__ballot(reset_env)) {
     if (reset_env) t = 0;
-    if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
+    if (M) {  // initial positions = the episode's first U pairs (draw table)
+      if (reset_env) drawn = U;
+      if (do_reset) {
+        const uint32_t row = (uint32_t)e * (uint32_t)M;
+        const int p = at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)u));
+        pos = make_int2((int)(short)p, p >> 16);
+        wp = make_int2(-1, -1);
+        if (u == U - 1) s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)u));
+      }
+    } else if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc = at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e + 32u);
       if (kp.movement_reseed) s = mk128(pc.x, pc.y);
       s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
@@ -456,12 +482,35 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
   const int rank = __popcll(mneed & lt);
   if (mneed_w) {
-    // common case: every drawing lane of the wave is the first of its env and no reset came
-    // before -> two steps of the constant multiplier instead of a table jump
-    if (__ballot(need && (rank | koff)) == 0) {
-      if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, wp.x, wp.y);
+    const int k = drawn + rank;  // this draw's pair index in the episode
+    if (M && __ballot(need && k >= M) == 0) {
+      // draw table: every drawing lane of the wavefront finds its pair precomputed
+      if (need) {
+        const uint32_t row = (uint32_t)e * (uint32_t)M;
+        const int p = at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)k));
+        wp = make_int2((int)(short)p, p >> 16);
+        if (rank == tot - 1) s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)k));
+      }
     } else {
-      if (need) s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
+      if (M) {  // beyond the table: from the stream state (loaded only on this path)
+        ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+        const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
+        inc = mk128(pb.x, pb.y);
+        s = mk128(pa.x, pa.y);
+        if (reset_env) {  // the state after this episode's U initial pairs
+          const u128 su = at(const_cast<u128*>(tb.tab_st),
+                             16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(U - 1)));
+          s = su;
+        }
+      }
+      // common case: every drawing lane of the wave is the first of its env and no reset
+      // came before -> two steps of the constant multiplier instead of a table jump
+      if (__ballot(need && (rank | koff)) == 0) {
+        if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, wp.x, wp.y);
+      } else {
+        if (need)
+          s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
+      }
     }
   }
   // owner of the env's new stream state: the last drawing lane, else (reset without draws)
@@ -580,6 +629,7 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
                          : kp.lower)
              : (nact > 0 ? sum_u / (double)nact : kp.lower);
     at(st.t, 4u * (uint32_t)e) = t + 1;
+    if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
     at(out.reward, 4u * (uint32_t)e) = (float)mean_u;
     at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
     if (want_metrics) {
@@ -627,7 +677,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const LaneMap m = lane_map<PC>(lane, P);
   const int e = g * G + m.seg;
   const bool env_ok = (m.seg < G) && (e < kp.E);
-  const GroupIn a = load_group(kp, st, e, min(m.u, U - 1), U);
+  const GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U);
   packed_group<PER_ENV_BS, LEAN, UC>(kp, st, out, tb, m, a, e, env_ok,
                                      lds_hist + (threadIdx.x >> 6) * G * kp.B);
 }
@@ -935,6 +985,26 @@ __global__ void k_assoc_map(const int2* __restrict__ bs, int B, int W, int H, in
   map[i] = r;
 }
 
+// Episode draw table of the envs with mask[e] (all if NULL): pair k of env e = draws 2k and
+// 2k + 1 of the stream re-seeded to state0 (what every episode of the env draws, in order),
+// and the stream state after them. One thread per (env, pair).
+__global__ void k_draw_table(KParams kp, const uint64_t* __restrict__ pcg,
+                             const uint8_t* __restrict__ mask, const u128* __restrict__ jump,
+                             int* __restrict__ tab_xy, u128* __restrict__ tab_st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int M = kp.tab_m;
+  if (i >= (int64_t)kp.E * M) return;
+  const int e = (int)(i / M), k = (int)(i - (int64_t)e * M);
+  if (mask != nullptr && !mask[e]) return;
+  const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(pcg + (size_t)6 * e);
+  const ulonglong2 pb = pr[1], pc = pr[2];
+  int x, y;
+  const u128 s2 = pcg_draw_pair(mk128(pc.x, pc.y), mk128(pb.x, pb.y), 2 * k, jump, kp.Wd, kp.Hd,
+                                x, y);
+  tab_xy[i] = (int)(((unsigned)x & 0xffffu) | ((unsigned)y << 16));
+  tab_st[i] = s2;
+}
+
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
 __global__ void k_jump_table(int kmax, u128* __restrict__ jump) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -971,6 +1041,9 @@ struct mev_ctx {
   double* util;
   int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
+  int* tab_xy;        // episode draw table (params.draw_table), see KTables
+  u128* tab_st;
+  int* drawn;
   hipStream_t aux;    // second stream of the two-half shape
   hipEvent_t ev_fork, ev_join;
 };
@@ -1118,8 +1191,25 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     return MEV_ECHANNEL;
   }
 
-  // ---- PCG64 jump table: offsets up to 2U (reset) + 2U (waypoints) ----
-  c->jmax = 4 * params->num_ues;
+  // ---- episode draw table (packed shape, movement re-seeded every episode) ----
+  c->kp.tab_m = 0;
+  if (params->draw_table != 0 && params->movement_reseed && params->num_ues <= 64)
+    c->kp.tab_m = params->draw_table > 0 ? params->draw_table : 4 * params->num_ues + 16;
+  if (c->kp.tab_m) {
+    const size_t n = (size_t)params->num_envs * (size_t)c->kp.tab_m;
+    if (c->kp.tab_m < params->num_ues || n >= ((size_t)1 << 28) ||
+        hipMalloc(&c->tab_xy, sizeof(int) * n) != hipSuccess ||
+        hipMalloc(&c->tab_st, sizeof(u128) * n) != hipSuccess ||
+        hipMalloc(&c->drawn, sizeof(int) * (size_t)params->num_envs) != hipSuccess) {
+      const bool bad = c->kp.tab_m < params->num_ues || n >= ((size_t)1 << 28);
+      mev_destroy(c);
+      return bad ? MEV_EINVAL : MEV_ENOMEM;
+    }
+    MEV_HIP(hipMemset(c->drawn, 0, sizeof(int) * (size_t)params->num_envs));
+  }
+
+  // ---- PCG64 jump table: offsets up to 2U (reset) + 2U (waypoints), and the table pairs --
+  c->jmax = max(4 * params->num_ues, 2 * c->kp.tab_m + 2);
   if (hipMalloc(&c->jump, sizeof(u128) * 2 * (size_t)(c->jmax + 1)) != hipSuccess) {
     mev_destroy(c);
     return MEV_ENOMEM;
@@ -1186,6 +1276,9 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
   if (c->assoc) (void)hipFree(c->assoc);
+  if (c->tab_xy) (void)hipFree(c->tab_xy);
+  if (c->tab_st) (void)hipFree(c->tab_st);
+  if (c->drawn) (void)hipFree(c->drawn);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1284,7 +1377,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util, c->assoc};
+  KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
@@ -1320,11 +1413,25 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   return MEV_OK;
 }
 
+int mev_prepare_draws(const mev_ctx* c, const mev_state* st, const uint8_t* env_mask,
+                      void* stream) {
+  if (!c || !st || !st->pcg) return MEV_EINVAL;
+  if (!c->kp.tab_m) return MEV_OK;
+  const int64_t n = (int64_t)c->kp.E * c->kp.tab_m;
+  hipLaunchKernelGGL(k_draw_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, c->kp, st->pcg, env_mask, c->jump, c->tab_xy,
+                     c->tab_st);
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
 int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
               const uint8_t* env_mask, void* stream) {
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   rc = mev_update_stations(c, st->bs_xy, stream);
+  if (rc) return rc;
+  rc = mev_prepare_draws(c, st, env_mask, stream);
   if (rc) return rc;
   return launch<true>(c, st, out, env_mask, (hipStream_t)stream);
 }
@@ -1338,7 +1445,7 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
     KState ks;
     KOut ko;
     to_kernel(st, out, ks, ko);
-    const KTables tb{c->rate_full, c->jump, c->util, c->assoc};
+    const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn};
     return launch_packed_steps(c, ks, ko, tb, nsteps, (hipStream_t)stream);
   }
   for (int i = 0; i < nsteps; ++i) {

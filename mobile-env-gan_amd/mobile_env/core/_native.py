@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -25,7 +25,7 @@ MEV_ECHANNEL = -1001
 EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations",
-           "mev_reset", "mev_step", "mev_strerror", "mev_last_hip_error")
+           "mev_reset", "mev_prepare_draws", "mev_step", "mev_strerror", "mev_last_hip_error")
 
 
 class MevParams(C.Structure):
@@ -34,7 +34,7 @@ class MevParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("ep_max_time", C.c_int32),
         ("arrival_start", C.c_int32), ("arrival_exit", C.c_int32),
         ("bs_per_env", C.c_int32), ("first_step_active", C.c_int32),
-        ("movement_reseed", C.c_int32), ("stream_split", C.c_int32),
+        ("movement_reseed", C.c_int32), ("draw_table", C.c_int32), ("stream_split", C.c_int32),
         ("velocity", C.c_double),
         ("bs_bw", C.c_double), ("bs_freq", C.c_double), ("bs_tx", C.c_double),
         ("bs_height", C.c_double),
@@ -97,6 +97,8 @@ def lib():
         L.mev_seed_pcg64.restype = C.c_int
         L.mev_seed_pcg64_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.mev_seed_pcg64_device.restype = C.c_int
+        L.mev_prepare_draws.argtypes = [C.c_void_p, C.POINTER(MevState), C.c_void_p, C.c_void_p]
+        L.mev_prepare_draws.restype = C.c_int
         L.mev_update_stations.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mev_update_stations.restype = C.c_int
         L.mev_reset.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),

@@ -53,6 +53,7 @@ class EngineParams:
     util_upper: float = 20.0
     util_coeffs: tuple = (10.0, 0.0, 10.0)
     stream_split: int = 0  # mev_params.stream_split: 0 auto, 1 single stream, 2 two halves
+    draw_table: int = -1   # mev_params.draw_table: episode draw table pairs per env (-1 auto)
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
 
     def to_c(self, bs_per_env: bool) -> N.MevParams:
@@ -62,7 +63,7 @@ class EngineParams:
             arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
             bs_per_env=int(bs_per_env), first_step_active=int(bool(self.first_step_active)),
             movement_reseed=int(bool(self.movement_reseed)),
-            stream_split=int(self.stream_split),
+            draw_table=int(self.draw_table), stream_split=int(self.stream_split),
             velocity=float(self.velocity),
             bs_bw=float(self.bs["bw"]), bs_freq=float(self.bs["freq"]),
             bs_tx=float(self.bs["tx"]), bs_height=float(self.bs["height"]),
@@ -144,8 +145,8 @@ class StepEngine:
             self.metrics = torch.zeros((E, 4), dtype=torch.float32, **kw) if metrics else None
             self.qoe_stats = (torch.zeros((E, 4), dtype=torch.float64, **kw) if qoe_stats
                               else None)
-        self.seed(seeds)
         self._bind()
+        self.seed(seeds)
         with torch.cuda.device(device):
             N.check(L.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),
                     "mev_update_stations")
@@ -209,6 +210,9 @@ class StepEngine:
             rows = N.seed_pcg64((s + 4).astype(np.uint64))
             self.pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
         self.t.fill_(self.p.t_end)
+        with torch.cuda.device(self.device):  # the episode draw tables follow the new streams
+            N.check(self._lib.mev_prepare_draws(self._ctx, C.byref(self._st), None,
+                                                self._stream()), "mev_prepare_draws")
 
     def set_bs_layout(self, bs_xy, bs_count=None):
         bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)

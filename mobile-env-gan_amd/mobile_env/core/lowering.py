@@ -62,4 +62,5 @@ def lower(*, num_envs, stations, users, arrival, channel, scheduler, movement, u
         velocity=float(uep[0]),
         bs={"bw": bsp[0], "freq": bsp[1], "tx": bsp[2], "height": bsp[3]},
         ue={"snr_tr": uep[1], "noise": uep[2], "height": uep[3]},
-        util_lower=ut["util_lower"], util_upper=ut["util_upper"], util_coeffs=ut["util_coeffs"])
+        util_lower=ut["util_lower"], util_upper=ut["util_upper"], util_coeffs=ut["util_coeffs"],
+        draw_table=0)  # the facade carries pcg / t across engine rebuilds: no episode table
