@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 5
+#define MEV_ABI_VERSION 6
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -81,6 +81,9 @@ typedef struct mev_params {
                                 env precomputed from state0 by mev_reset / mev_prepare_draws
                                 (every episode of an env draws the same sequence); -1 auto
                                 (4U + 16), 0 off */
+  int32_t fuse_steps;        /* mev_step(n > 1), U <= 64: 0 (auto) -> the n steps run in ONE
+                                launch with the env state in registers between them (outputs
+                                written every step, identical results); -1: n launches */
   int32_t stream_split;      /* mev_step launch shape: 0 (auto) or 1: one kernel per step on
                                 the caller's stream; 2: the env batch in two halves on the
                                 caller's stream and a context-owned stream (joined before

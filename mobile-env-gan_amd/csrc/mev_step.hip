@@ -139,6 +139,11 @@ __device__ __forceinline__ uint64_t pcg_output(u128 s) {
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
 
+__device__ __forceinline__ u128 shfl_u128(u128 v, int src) {
+  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+  return mk128(__shfl(lo, src), __shfl(hi, src));
+}
+
 // numpy Generator.uniform(0, span) is off + scale * next_double with next_double =
 // (next_uint64 >> 11) * 2^-53 (numpy/random/src/distributions/distributions.c); the reference
 // then truncates with int() (movement.py:45-46,67-68). PCG64 advances, then outputs.
@@ -356,18 +361,19 @@ struct GroupIn {
 };
 
 __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st,
-                                              const KTables& tb, int e, int u, int U) {
+                                              const KTables& tb, int e, int u, int U,
+                                              bool fused) {
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue(&at(st.ue_state, 8u * ue));
-  if (kp.tab_m) {  // the stream state is read only when a draw falls beyond the table
+  if (kp.tab_m && !fused) {  // the stream state is read only when a draw falls beyond the table
     g.drawn = at(tb.drawn, 4u * (uint32_t)ec);
     g.pa = g.pb = make_ulonglong2(0, 0);
   } else {
     ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-    g.drawn = 0;
+    g.drawn = kp.tab_m ? at(tb.drawn, 4u * (uint32_t)ec) : 0;
     g.pa = at(pr, 48u * (uint32_t)ec);
     g.pb = at(pr, 48u * (uint32_t)ec + 16u);
   }
@@ -415,10 +421,13 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
 //         reductions and the env indexing for the registered scenario sizes;
 //   LEAN: no float64 rate / utility / metrics outputs and the utility in its float32 form
 //         (the Gym surface's default), so none of the optional work is even branched over.
-template <bool PER_ENV_BS, bool LEAN, int UC>
-__device__ __forceinline__ void packed_group(const KParams& kp, const KState& st,
+//   FUSED: one of several steps of a launch (mev_step(n), n > 1): the env state stays in
+//         registers between the steps (`cur` is updated; the caller stores it after the last
+//         step), the per-step outputs are written every step as in separate launches.
+template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED>
+__device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
-                                             const LaneMap& m, const GroupIn& cur, int e,
+                                             const LaneMap& m, GroupIn& cur, int e,
                                              bool env_ok, int* __restrict__ hist) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
@@ -493,10 +502,12 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       }
     } else {
       if (M) {  // beyond the table: from the stream state (loaded only on this path)
-        ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-        const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
-        inc = mk128(pb.x, pb.y);
-        s = mk128(pa.x, pa.y);
+        if (!FUSED) {  // fused steps carry the state in registers
+          ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+          const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
+          inc = mk128(pb.x, pb.y);
+          s = mk128(pa.x, pa.y);
+        }
         if (reset_env) {  // the state after this episode's U initial pairs
           const u128 su = at(const_cast<u128*>(tb.tab_st),
                              16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(U - 1)));
@@ -516,6 +527,15 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   // owner of the env's new stream state: the last drawing lane, else (reset without draws)
   // the last UE's lane, else nobody (the stream did not move)
   const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
+  if (FUSED) {  // every lane of an env whose stream moved takes the owner's new state
+    const uint64_t mown = __ballot(own_fin);
+    if (mown) {
+      const uint64_t segown = mown & segmask;
+      const int src = segown ? 63 - __clzll((unsigned long long)segown) : __lane_id();
+      const u128 sb = shfl_u128(s_fin, src);
+      if (segown) s = sb;
+    }
+  }
   if (active) move_ue(pos, wp, kp);
 
   // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
@@ -612,11 +632,11 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
   // ---- 6. stores ----------------------------------------------------------------------
   if (valid) {
     const uint32_t ui = (uint32_t)idx;
-    store_ue(&at(st.ue_state, 8u * ui), pos, wp);
+    if (!FUSED) store_ue(&at(st.ue_state, 8u * ui), pos, wp);
     at(out.serving, 4u * ui) = srv;
     at(out.obs, 16u * ui) = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
                                         (float)cents * 0.01f, (float)util);
-    if (own_fin)  // the stream moved (draws, or reset): write the new state back
+    if (!FUSED && own_fin)  // the stream moved (draws, or reset): write the new state back
       at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) =
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
@@ -628,8 +648,10 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
         LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
                          : kp.lower)
              : (nact > 0 ? sum_u / (double)nact : kp.lower);
-    at(st.t, 4u * (uint32_t)e) = t + 1;
-    if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
+    if (!FUSED) {
+      at(st.t, 4u * (uint32_t)e) = t + 1;
+      if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
+    }
     at(out.reward, 4u * (uint32_t)e) = (float)mean_u;
     at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
     if (want_metrics) {
@@ -646,6 +668,14 @@ __device__ __forceinline__ void packed_group(const KParams& kp, const KState& st
       out.qoe_stats[e] = a;
     }
   }
+  if (FUSED) {
+    cur.t = t + 1;
+    cur.s = make_int4(pos.x, pos.y, wp.x, wp.y);
+    cur.drawn = drawn + tot;
+    cur.pa = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
+    cur.pb = make_ulonglong2((uint64_t)inc, (uint64_t)(inc >> 64));
+  }
+  return __ballot(own_fin) & segmask;  // the env's stream moved this step
 }
 
 // Block -> env-range slot. Blocks are dealt round-robin over the 8 XCDs (observed placement,
@@ -677,9 +707,46 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const LaneMap m = lane_map<PC>(lane, P);
   const int e = g * G + m.seg;
   const bool env_ok = (m.seg < G) && (e < kp.E);
-  const GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U);
-  packed_group<PER_ENV_BS, LEAN, UC>(kp, st, out, tb, m, a, e, env_ok,
-                                     lds_hist + (threadIdx.x >> 6) * G * kp.B);
+  GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
+  packed_group<PER_ENV_BS, LEAN, UC, false>(kp, st, out, tb, m, a, e, env_ok,
+                                            lds_hist + (threadIdx.x >> 6) * G * kp.B);
+}
+
+// nsteps fused steps per launch (mev_step(n), n > 1): each wavefront advances its env group
+// n steps with the state in registers -- loaded once, stored once -- and writes the step
+// outputs of every step (as n launches would; the caller sees the last step's). One launch
+// instead of n removes n - 1 kernel boundaries and the fill / drain of every launch.
+template <bool PER_ENV_BS, bool LEAN, int UC>
+__global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KState st, KOut out,
+                                                              KTables tb, int ngroups,
+                                                              int nsteps) {
+  extern __shared__ int lds_hist[];
+  const int lane = threadIdx.x & 63;
+  const int g = block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  constexpr int PC = UC ? pitch_of(UC) : 0;
+  constexpr bool ROWS = PC == 16 || PC == 32;
+  const int U = UC ? UC : kp.U;
+  const int P = PC ? PC : kp.U;
+  const int G = PC ? 64 / (PC ? PC : 1) : kp.envs_per_wave;
+  const LaneMap m = lane_map<PC>(lane, P);
+  const int e = g * G + m.seg;
+  const bool env_ok = (m.seg < G) && (e < kp.E);
+  int* hist = lds_hist + (threadIdx.x >> 6) * G * kp.B;
+  GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
+  bool moved = false;
+  for (int i = 0; i < nsteps; ++i)
+    moved |= packed_group<PER_ENV_BS, LEAN, UC, true>(kp, st, out, tb, m, a, e, env_ok, hist);
+  // the state after the last step
+  if (env_ok && m.u < U)
+    store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
+             make_int2(a.s.z, a.s.w));
+  const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
+  if (env_ok && leader) {
+    at(st.t, 4u * (uint32_t)e) = a.t;
+    if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
+    if (moved) at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) = a.pa;
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1041,6 +1108,7 @@ struct mev_ctx {
   double* util;
   int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
+  int fuse_steps;     // mev_step(n > 1): one fused launch (params.fuse_steps)
   int* tab_xy;        // episode draw table (params.draw_table), see KTables
   u128* tab_st;
   int* drawn;
@@ -1259,6 +1327,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   //      dispatches cannot be timed one by one)
   c->parts = 1;
   if (c->kp.U <= 64 && params->stream_split == 2) c->parts = 2;
+  c->fuse_steps = params->fuse_steps >= 0;
   if (c->parts == 2) {
     MEV_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     MEV_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
@@ -1337,6 +1406,23 @@ static StepKernel step_kernel_for(bool per_env, bool lean, int U) {
   return lean ? step_kernel_u<false, true>(U) : step_kernel_u<false, false>(U);
 }
 
+typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int);
+
+template <bool PER_ENV_BS, bool LEAN>
+static StepsKernel steps_kernel_u(int U) {
+  switch (U) {
+    case 5: return k_steps_packed<PER_ENV_BS, LEAN, 5>;
+    case 15: return k_steps_packed<PER_ENV_BS, LEAN, 15>;
+    case 30: return k_steps_packed<PER_ENV_BS, LEAN, 30>;
+    default: return k_steps_packed<PER_ENV_BS, LEAN, 0>;
+  }
+}
+
+static StepsKernel steps_kernel_for(bool per_env, bool lean, int U) {
+  if (per_env) return lean ? steps_kernel_u<true, true>(U) : steps_kernel_u<true, false>(U);
+  return lean ? steps_kernel_u<false, true>(U) : steps_kernel_u<false, false>(U);
+}
+
 // Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
 // the caller's stream, the second on c->aux (forked from and joined back into the caller's
 // stream); the halves are independent envs, so the two streams overlap freely.
@@ -1348,6 +1434,14 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   const StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
   const size_t shmem =
       kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;
+  // n > 1 steps on one stream: one launch of the fused multi-step kernel
+  if (nsteps > 1 && c->parts == 1 && c->fuse_steps) {
+    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
+    const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    kf<<<dim3(blocks), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, groups, nsteps);
+    MEV_HIP(hipGetLastError());
+    return MEV_OK;
+  }
   // split on a block boundary
   const int half = (groups / 2 + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
   if (c->parts == 1 || half <= 0 || half >= groups) {

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -34,7 +34,8 @@ class MevParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("ep_max_time", C.c_int32),
         ("arrival_start", C.c_int32), ("arrival_exit", C.c_int32),
         ("bs_per_env", C.c_int32), ("first_step_active", C.c_int32),
-        ("movement_reseed", C.c_int32), ("draw_table", C.c_int32), ("stream_split", C.c_int32),
+        ("movement_reseed", C.c_int32), ("draw_table", C.c_int32), ("fuse_steps", C.c_int32),
+        ("stream_split", C.c_int32),
         ("velocity", C.c_double),
         ("bs_bw", C.c_double), ("bs_freq", C.c_double), ("bs_tx", C.c_double),
         ("bs_height", C.c_double),

@@ -54,6 +54,7 @@ class EngineParams:
     util_coeffs: tuple = (10.0, 0.0, 10.0)
     stream_split: int = 0  # mev_params.stream_split: 0 auto, 1 single stream, 2 two halves
     draw_table: int = -1   # mev_params.draw_table: episode draw table pairs per env (-1 auto)
+    fuse_steps: int = 0    # mev_params.fuse_steps: 0 step(n > 1) in one launch, -1 n launches
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
 
     def to_c(self, bs_per_env: bool) -> N.MevParams:
@@ -63,7 +64,8 @@ class EngineParams:
             arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
             bs_per_env=int(bs_per_env), first_step_active=int(bool(self.first_step_active)),
             movement_reseed=int(bool(self.movement_reseed)),
-            draw_table=int(self.draw_table), stream_split=int(self.stream_split),
+            draw_table=int(self.draw_table), fuse_steps=int(self.fuse_steps),
+            stream_split=int(self.stream_split),
             velocity=float(self.velocity),
             bs_bw=float(self.bs["bw"]), bs_freq=float(self.bs["freq"]),
             bs_tx=float(self.bs["tx"]), bs_height=float(self.bs["height"]),
