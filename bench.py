@@ -6,17 +6,23 @@ Contract (see DESIGN.md "Measurement"):
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 
-* One step = one launch of the fused step kernel over every env on the GPU (BASELINE.json
-  configs[2]: 65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank
-  owns its own 65,536 independent envs, seeds 1000 + global env index).
+* One step = one pass of the step over every env on the GPU (BASELINE.json configs[2]:
+  65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank owns its own
+  65,536 independent envs, seeds 1000 + global env index). Steps are issued as
+  ``engine.step(20)`` (mev_step with n = 20, one episode): by default ONE launch of the fused
+  multi-step kernel, which keeps every env's state in registers between the 20 steps and
+  writes every step's outputs (obs, serving, reward, done), bit-identical to 20 launches;
+  ``--launch single`` issues 20 one-step launches instead.
 * Timed region: barrier + synchronize, K steps, the single final all-gather of the
   (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
   ranks time. Inputs are resident in HBM before timing starts.
-* roofline: algorithmic bytes per launch = E * (54*U + 61) over the kernel's
-  average duration, measured with HIP events on the stream the kernel runs on, recorded
-  around every chunk of 20 back-to-back launches (the average includes the gaps between
-  launches). traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
-  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
+* roofline: algorithmic bytes per launch = E * (54*U + 61) x steps per launch,
+  over the launch's average duration from HIP events on the stream the kernel runs on
+  (around every launch; for one-step launches around every chunk of 20, gaps included).
+  traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
+  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null --
+  below the algorithmic bytes because the state is 8 B per UE (canonical: 34 B) and, fused,
+  makes one round trip per launch instead of one per step.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
   per core, run before the GPU is touched.
@@ -79,18 +85,18 @@ def cpu_baseline(budget_s: float, procs: int):
                        f"(no JSON dump): {steps} env-steps in {wall:.1f} s")}
 
 
-def load_profile(workload: str, envs: int):
-    """(HBM bytes per launch from the PMC passes, rocprofv3 average step-kernel duration in
-    ms) of the committed profile of this workload (tools/profile.sh + tools/pmc_summary.py),
-    or Nones."""
+def load_profile(workload: str, envs: int, launch: str = "fused"):
+    """(HBM bytes per launch from the PMC passes, rocprofv3 average launch duration in ms of
+    the timed region) of the committed profile of this workload and launch shape
+    (tools/profile.sh + tools/pmc_summary.py), or Nones."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
-    ent = d.get(f"{workload}@{envs}") or {}
-    avg_ns = ent.get("rocprof_kernel_avg_ns")
+    ent = d.get(f"{workload}@{envs}@{launch}") or {}
+    avg_ns = ent.get("rocprof_launch_avg_ns")
     return ent.get("hbm_bytes_per_launch"), (avg_ns * 1e-6 if avg_ns else None)
 
 
@@ -102,8 +108,9 @@ def main():
     ap.add_argument("--workload", default="mobile-large-central-v0")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--stream-split", type=int, default=0, choices=(0, 1, 2),
-                    help="mev_params.stream_split (2: two env halves on two HIP streams)")
+    ap.add_argument("--launch", default="fused", choices=("fused", "single", "split"),
+                    help="fused: 20 steps per launch (default); single: one launch per step; "
+                         "split: one launch per step on two HIP streams (two env halves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
@@ -143,24 +150,25 @@ def main():
     E = args.envs
     seeds = shard_seeds(1000, E, rank)  # rank r owns global envs [r*E, (r+1)*E)
     env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
-                          stream_split=args.stream_split)
+                          stream_split=2 if args.launch == "split" else 0,
+                          fuse_steps=0 if args.launch == "fused" else -1)
     U, B = env.num_ues, env.num_bs
     per_env_bs = env.engine.bs_per_env
     parts = env.engine.launch_parts
     env.reset()
-    # warmup (also brings the GPU to its steady clock): the Gym step once, then C-loop chunks
+    CHUNK = 20  # steps per engine.step call (one episode)
+    # warmup (also brings the GPU to its steady clock): the Gym step once, then chunks
     if args.warmup > 0:
         env.step()
-        env.engine.step(args.warmup - 1)
+        for _ in range(-(-(args.warmup - 1) // CHUNK)):
+            env.engine.step(CHUNK)
     torch.cuda.synchronize(device)
 
-    # Steps are issued in chunks of CHUNK back-to-back launches from C (mev_step loops over
-    # launches; a Python call per step would make the host, not the GPU, the bottleneck),
+    # Steps are issued in chunks of CHUNK from C (fused: one launch per chunk; single: CHUNK
+    # back-to-back launches -- a Python call per step would make the host the bottleneck),
     # with a HIP event pair around every chunk on the caller's stream. With the two-half
-    # launch shape (mev_params.stream_split) the second half runs on the context's own
-    # stream and is joined back before mev_step returns, so each event pair brackets whole
-    # steps of the full batch.
-    CHUNK = 20
+    # launch shape the second half runs on the context's own stream and is joined back
+    # before mev_step returns, so each event pair brackets whole steps of the full batch.
     K = -(-args.steps // CHUNK) * CHUNK
     stream = torch.cuda.current_stream(device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -190,9 +198,12 @@ def main():
     if rank == 0:
         value = world * E * K / elapsed
         bpe = algorithmic_bytes_per_env_step(U, per_env_bs, B)
-        algo_bytes = E * bpe
-        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, rocprof_ms = load_profile(args.workload, E)
+        fused = args.launch == "fused" and env.engine.fused_steps
+        spl = CHUNK if fused else 1  # steps per launch
+        algo_bytes = E * bpe * spl
+        launch_ms = kern_ms * spl
+        achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+        traffic, rocprof_ms = load_profile(args.workload, E, args.launch)
         out = {
             "metric": METRIC,
             "value": value,
@@ -212,11 +223,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
+                         "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                          if traffic else None),
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "kernel_ms": kern_ms,
-                         "rocprof_kernel_ms": rocprof_ms,
-                         "launch_shape": (f"{parts} halves per step on {parts} HIP streams"
-                                          if parts > 1 else "one kernel per step")},
+                         "steps_per_launch": spl,
+                         "launch_ms": launch_ms,
+                         "rocprof_launch_ms": rocprof_ms,
+                         "launch_shape": (
+                             f"fused: {spl} steps per launch, env state in registers between "
+                             f"them, outputs written every step" if fused else
+                             f"{parts} halves per step on {parts} HIP streams" if parts > 1
+                             else "one kernel per step")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

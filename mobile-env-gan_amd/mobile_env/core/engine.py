@@ -179,6 +179,11 @@ class StepEngine:
         return int(self._lib.mev_d2max(self._ctx))
 
     @property
+    def fused_steps(self) -> bool:
+        """step(n > 1) runs as one fused launch (U <= 64 and fuse_steps >= 0)."""
+        return self.p.num_ues <= 64 and self.p.fuse_steps >= 0
+
+    @property
     def launch_parts(self) -> int:
         """Env halves per step launch (1, or 2 on two streams)."""
         return int(self._lib.mev_launch_parts(self._ctx))

@@ -11,4 +11,5 @@ cat gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 tools/profile.sh ${PROFILE_TAG:-dev} || exit 1
+tools/profile.sh ${PROFILE_TAG:-dev}_single --launch single || exit 1
 

@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into profiles/ (committed evidence).
 
+usage: python tools/pmc_summary.py gpurun_out/prof_TAG TAG "<bench args of the profile run>"
+
 Reads the rocprofv3 CSVs of the passes (kt: kernel trace + stats; fetch / write / sq / sq2: PMC
-counters), keeps the STEP kernel dispatches (k_step_packed / k_step_block, RESET=false), and
-writes:
+counters) and keeps the dispatches of the launch the bench times:
+  * --launch fused (default): the fused multi-step kernel k_steps_packed (20 steps each);
+  * --launch single / split: the one-step kernels k_step_packed / k_step_block.
+Writes
   profiles/<tag>_kernel_stats.csv   -- rocprofv3 --stats summary (copied)
-  profiles/<tag>_pmc.json           -- per-launch averages of every counter
-  profiles/pmc_traffic.json         -- {workload@envs: hbm_bytes_per_launch, ...} read by bench.py
+  profiles/<tag>_pmc.json           -- per-launch averages of every counter, timed-region
+                                       launch durations from the trace, HBM bytes per launch
+  profiles/pmc_traffic.json         -- {workload@envs@launch: {...}} read by bench.py
 HBM bytes follow MI355X_MICROARCH.md section HBM: FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports half
 of a wide streaming read) + WRITE_SIZE (KB) x 1024.
 """
@@ -19,108 +24,100 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHUNK = 20  # bench.py: steps per engine.step call
+
+FUSED_RE = re.compile(r"k_steps_packed<")
+SINGLE_RE = re.compile(r"k_step_packed<|k_step_block<(true|false), false>")
 
 
-STEP_RE = re.compile(r"k_step_packed<|k_step_block<(true|false), false>")
-
-
-def is_step_kernel(name: str) -> bool:
-    return STEP_RE.search(name) is not None
-
-
-def counters(path_glob):
-    vals = {}
+def rows_of(path_glob, name_key):
     for path in glob.glob(path_glob, recursive=True):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if not is_step_kernel(row.get("Kernel_Name", "")):
-                    continue
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
-
-
-def step_interval(trace_glob, steps):
-    """From the kernel trace: step-kernel dispatches of the timed region (the last
-    steps x parts), their average duration, and the step interval = (last end - first start)
-    / steps -- with two halves per step on two streams the dispatch durations overlap, so
-    the interval, not the duration, is the time of a step."""
-    rows = []
-    for path in glob.glob(trace_glob, recursive=True):
-        with open(path) as f:
-            for row in csv.DictReader(f):
-                if is_step_kernel(row.get("Kernel_Name", "")):
-                    rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
-    if not rows or not steps:
-        return None
-    rows.sort()
-    return rows, steps
+            yield from csv.DictReader(f)
 
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
     extra = sys.argv[3] if len(sys.argv) > 3 else ""
-    prof = os.path.join(ROOT, "profiles")
-    os.makedirs(prof, exist_ok=True)
-    stats = glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)
-    step_avg_ns = None
-    if stats:
-        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-        with open(stats[0]) as f:
-            for row in csv.DictReader(f):
-                if is_step_kernel(row["Name"]):
-                    step_avg_ns = float(row["AverageNs"])
-    pmc = {}
-    ndisp = {}
-    for name in ("fetch", "write", "sq", "sq2"):
-        v, n = counters(os.path.join(out, name, "**", "*counter_collection.csv"))
-        pmc.update(v)
-        ndisp.update(n)
-    workload, envs, steps, warmup = "mobile-large-central-v0", 65536, 0, 0
+    workload, envs, steps, warmup, launch = "mobile-large-central-v0", 65536, 0, 0, "fused"
     toks = extra.split()
-    for i, t in enumerate(toks):
+    for i, t in enumerate(toks[:-1]):
         if t == "--workload":
             workload = toks[i + 1]
-        if t == "--envs":
+        elif t == "--envs":
             envs = int(toks[i + 1])
-        if t == "--steps":
+        elif t == "--steps":
             steps = int(toks[i + 1])
-        if t == "--warmup":
+        elif t == "--warmup":
             warmup = int(toks[i + 1])
-    summary = {"tag": tag, "workload": workload, "envs": envs, "bench_args": extra,
-               "step_kernel_avg_ns": step_avg_ns, "counters_per_launch": pmc,
-               "dispatches_sampled": ndisp}
-    tr = step_interval(os.path.join(out, "kt", "**", "*kernel_trace.csv"), steps)
-    parts = 1
-    if tr:
-        rows, _ = tr
-        total_steps = steps + warmup
-        parts = max(1, round(len(rows) / total_steps))
-        timed = rows[-steps * parts:]
+        elif t == "--launch":
+            launch = toks[i + 1]
+    kre = FUSED_RE if launch == "fused" else SINGLE_RE
+    steps = -(-steps // CHUNK) * CHUNK  # bench.py rounds up to whole chunks
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+
+    summary = {"tag": tag, "workload": workload, "envs": envs, "launch": launch,
+               "bench_args": extra}
+    stats = glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+        for row in rows_of(stats[0], "Name"):
+            if kre.search(row["Name"]):
+                summary["kernel"] = row["Name"].split("(")[0]
+                summary["stats_avg_ns"] = float(row["AverageNs"])
+                summary["stats_calls"] = int(row["Calls"])
+
+    # timed region from the trace: the last launches of the kernel
+    trace = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                   for r in rows_of(os.path.join(out, "kt", "**", "*kernel_trace.csv"), "")
+                   if kre.search(r.get("Kernel_Name", "")))
+    steps_per_launch = CHUNK if launch == "fused" else 1
+    parts = 2 if launch == "split" else 1
+    n_timed = steps // steps_per_launch * parts
+    if trace and n_timed:
+        timed = trace[-n_timed:]
         span = max(e for _, e in timed) - timed[0][0]
-        summary["launch_parts"] = parts
-        summary["timed_dispatches"] = len(timed)
-        summary["timed_dispatch_avg_ns"] = sum(e - b for b, e in timed) / len(timed)
+        summary["steps_per_launch"] = steps_per_launch
+        summary["timed_launches"] = len(timed)
+        summary["timed_launch_avg_ns"] = sum(e - b for b, e in timed) / len(timed)
         summary["step_interval_ns"] = span / steps
+
+    # counters: per-dispatch averages over the kernel's dispatches of each pass (the fused
+    # warmup launches are whole 20-step chunks too, so every dispatch is the same work)
+    pmc, ndisp = {}, {}
+    for name in ("fetch", "write", "sq", "sq2"):
+        vals = {}
+        for r in rows_of(os.path.join(out, name, "**", "*counter_collection.csv"), ""):
+            if kre.search(r.get("Kernel_Name", "")):
+                vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        for k, v in vals.items():
+            pmc[k] = sum(v) / len(v)
+            ndisp[k] = len(v)
+    summary["counters_per_launch"] = pmc
+    summary["dispatches_sampled"] = ndisp
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-        # per step = per dispatch x halves per step (the halves are equal-sized)
         fetch = pmc["FETCH_SIZE"] * 1024 * 2 * parts
         write = pmc["WRITE_SIZE"] * 1024 * parts
         summary["hbm_bytes_per_launch"] = fetch + write
-        summary["hbm_bytes_per_step"] = fetch + write
+        summary["hbm_bytes_per_step"] = (fetch + write) / steps_per_launch
         summary["fetch_bytes_per_launch_corrected"] = fetch
         summary["write_bytes_per_launch"] = write
+    if "SQ_INSTS_VALU" in pmc and pmc.get("SQ_WAVES"):
+        summary["valu_per_wave_per_step"] = pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"] / steps_per_launch
+        summary["salu_per_wave_per_step"] = pmc["SQ_INSTS_SALU"] / pmc["SQ_WAVES"] / steps_per_launch
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=2)
+
     tpath = os.path.join(prof, "pmc_traffic.json")
-    traffic = {}
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))
+    traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     if "hbm_bytes_per_launch" in summary:
-        traffic[f"{workload}@{envs}"] = {
+        traffic[f"{workload}@{envs}@{launch}"] = {
             "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
             "fetch_bytes_per_launch_corrected": summary["fetch_bytes_per_launch_corrected"],
             "write_bytes_per_launch": summary["write_bytes_per_launch"],
-            "rocprof_kernel_avg_ns": summary.get("step_kernel_avg_ns"),
+            "steps_per_launch": steps_per_launch,
+            "rocprof_launch_avg_ns": summary.get("timed_launch_avg_ns"),
             "source": f"profiles/{tag}_pmc.json"}
         with open(tpath, "w") as f:
             json.dump(traffic, f, indent=2)
