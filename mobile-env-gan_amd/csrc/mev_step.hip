@@ -356,6 +356,7 @@ __device__ __forceinline__ LaneMap lane_map(int lane, int P) {
 struct GroupIn {
   int t;
   int drawn;           // draw-table mode: pairs of the episode consumed so far
+  bool s_ok;           // fused + draw table: pa holds the state after pair drawn - 1
   int4 s;              // {x, y, wx, wy}
   ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
 };
@@ -366,6 +367,7 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
+  g.s_ok = true;
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue(&at(st.ue_state, 8u * ue));
   if (kp.tab_m && !fused) {  // the stream state is read only when a draw falls beyond the table
@@ -428,7 +430,8 @@ template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
-                                             bool env_ok, int* __restrict__ hist) {
+                                             bool env_ok, int* __restrict__ hist,
+                                             const int* __restrict__ ltab = nullptr) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   const int U = UC ? UC : kp.U;
@@ -449,6 +452,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   u128 s = mk128(cur.pa.x, cur.pa.y);
   const int M = kp.tab_m;  // wave-uniform
   int drawn = cur.drawn;
+  bool s_ok = cur.s_ok;
 
   // Stream bookkeeping without cross-lane moves: the step's waypoint draws start at offset
   // koff of stream state `s` (koff = 2U right after a reset: the initial positions took the
@@ -466,10 +470,12 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       if (reset_env) drawn = U;
       if (do_reset) {
         const uint32_t row = (uint32_t)e * (uint32_t)M;
-        const int p = at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)u));
+        const int p = FUSED ? ltab[m.seg * M + u]
+                            : at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)u));
         pos = make_int2((int)(short)p, p >> 16);
         wp = make_int2(-1, -1);
-        if (u == U - 1) s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)u));
+        if (!FUSED && u == U - 1)
+          s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)u));
       }
     } else if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc = at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e + 32u);
@@ -490,23 +496,31 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   const uint64_t mneed = mneed_w & segmask;
   const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
   const int rank = __popcll(mneed & lt);
+  bool fell_back = false;  // wave-uniform: this step's draws came from the stream state
   if (mneed_w) {
     const int k = drawn + rank;  // this draw's pair index in the episode
     if (M && __ballot(need && k >= M) == 0) {
-      // draw table: every drawing lane of the wavefront finds its pair precomputed
+      // draw table: every drawing lane of the wavefront finds its pair precomputed (fused
+      // launches read the wavefront's copy in LDS and track only `drawn`)
       if (need) {
         const uint32_t row = (uint32_t)e * (uint32_t)M;
-        const int p = at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)k));
+        const int p = FUSED ? ltab[m.seg * M + k]
+                            : at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)k));
         wp = make_int2((int)(short)p, p >> 16);
-        if (rank == tot - 1) s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)k));
+        if (!FUSED && rank == tot - 1)
+          s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)k));
       }
     } else {
-      if (M) {  // beyond the table: from the stream state (loaded only on this path)
-        if (!FUSED) {  // fused steps carry the state in registers
+      fell_back = true;
+      if (M) {  // beyond the table: from the stream state
+        if (!FUSED) {  // loaded only on this path
           ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
           const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
           inc = mk128(pb.x, pb.y);
           s = mk128(pa.x, pa.y);
+        } else if (!s_ok && drawn > 0) {  // fused: the registers may trail the table draws
+          s = at(const_cast<u128*>(tb.tab_st),
+                 16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(min(drawn, M) - 1)));
         }
         if (reset_env) {  // the state after this episode's U initial pairs
           const u128 su = at(const_cast<u128*>(tb.tab_st),
@@ -527,13 +541,19 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // owner of the env's new stream state: the last drawing lane, else (reset without draws)
   // the last UE's lane, else nobody (the stream did not move)
   const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
-  if (FUSED) {  // every lane of an env whose stream moved takes the owner's new state
-    const uint64_t mown = __ballot(own_fin);
-    if (mown) {
-      const uint64_t segown = mown & segmask;
-      const int src = segown ? 63 - __clzll((unsigned long long)segown) : __lane_id();
-      const u128 sb = shfl_u128(s_fin, src);
-      if (segown) s = sb;
+  if (FUSED) {
+    if (!M || fell_back) {  // every lane of an env whose stream moved takes the new state
+      const uint64_t mown = __ballot(own_fin);
+      if (mown) {
+        const uint64_t segown = mown & segmask;
+        const int src = segown ? 63 - __clzll((unsigned long long)segown) : __lane_id();
+        const u128 sb = shfl_u128(s_fin, src);
+        if (segown) s = sb;
+      }
+    }
+    if (M) {  // with the table, the registers hold the state only after a fallback draw
+      if (fell_back && tot > 0) s_ok = true;
+      else if (tot > 0 || reset_env) s_ok = false;
     }
   }
   if (active) move_ue(pos, wp, kp);
@@ -672,6 +692,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cur.t = t + 1;
     cur.s = make_int4(pos.x, pos.y, wp.x, wp.y);
     cur.drawn = drawn + tot;
+    cur.s_ok = s_ok;
     cur.pa = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
     cur.pb = make_ulonglong2((uint64_t)inc, (uint64_t)(inc >> 64));
   }
@@ -732,11 +753,23 @@ __global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KStat
   const LaneMap m = lane_map<PC>(lane, P);
   const int e = g * G + m.seg;
   const bool env_ok = (m.seg < G) && (e < kp.E);
-  int* hist = lds_hist + (threadIdx.x >> 6) * G * kp.B;
+  const int wv = threadIdx.x >> 6;
+  int* hist = lds_hist + wv * G * kp.B * kp.hist_lds;
+  // the group's episode draw tables (x, y pairs) in LDS for the whole launch
+  int* ltab = lds_hist + kWavesPerBlock * G * kp.B * kp.hist_lds + wv * G * kp.tab_m;
+  if (kp.tab_m) {
+    const int n = G * kp.tab_m;
+    const int* src = tb.tab_xy + (size_t)g * n;
+    const int lim = (kp.E - g * G) * kp.tab_m;  // rows of envs that exist
+    for (int i = lane; i < n; i += 64)
+      if (i < lim) ltab[i] = src[i];
+    __builtin_amdgcn_wave_barrier();
+  }
   GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
   bool moved = false;
   for (int i = 0; i < nsteps; ++i)
-    moved |= packed_group<PER_ENV_BS, LEAN, UC, true>(kp, st, out, tb, m, a, e, env_ok, hist);
+    moved |= packed_group<PER_ENV_BS, LEAN, UC, true>(kp, st, out, tb, m, a, e, env_ok, hist,
+                                                      ltab);
   // the state after the last step
   if (env_ok && m.u < U)
     store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
@@ -745,7 +778,13 @@ __global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KStat
   if (env_ok && leader) {
     at(st.t, 4u * (uint32_t)e) = a.t;
     if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
-    if (moved) at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) = a.pa;
+    if (moved) {  // the state after the last pair drawn
+      const ulonglong2 sf =
+          a.s_ok ? a.pa
+                 : at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
+                      16u * ((uint32_t)e * (uint32_t)kp.tab_m + (uint32_t)(a.drawn - 1)));
+      at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) = sf;
+    }
   }
 }
 
@@ -1438,7 +1477,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   if (nsteps > 1 && c->parts == 1 && c->fuse_steps) {
     const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
     const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    kf<<<dim3(blocks), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, groups, nsteps);
+    const size_t shmem_f =
+        shmem + sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.tab_m;
+    kf<<<dim3(blocks), dim3(kPackedBlock), shmem_f, stream>>>(kp, ks, ko, tb, groups, nsteps);
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }
