@@ -8,21 +8,23 @@ Contract (see DESIGN.md "Measurement"):
 
 * One step = one pass of the step over every env on the GPU (BASELINE.json configs[2]:
   65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank owns its own
-  65,536 independent envs, seeds 1000 + global env index). Steps are issued as
-  ``engine.step(20)`` (mev_step with n = 20, one episode): by default ONE launch of the fused
-  multi-step kernel, which keeps every env's state in registers between the 20 steps and
-  writes every step's outputs (obs, serving, reward, done), bit-identical to 20 launches;
-  ``--launch single`` issues 20 one-step launches instead.
+  65,536 independent envs, seeds 1000 + global env index). By default steps are issued as
+  ``engine.rollout(20, traj)`` (mev_rollout, one episode): ONE launch of the fused multi-step
+  kernel, which keeps every env's state in registers between the 20 steps and writes EVERY
+  step's outputs (obs, serving, reward, done) to its own row of a [20, E, ...] trajectory
+  buffer in HBM -- the per-step outputs the reference's driver consumes every step
+  (base.py:261) -- bit-identical to 20 one-step launches. ``--launch single`` issues 20
+  one-step launches (mev_step(1), outputs overwritten) instead; ``split`` two env halves.
 * Timed region: barrier + synchronize, K steps, the single final all-gather of the
   (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
   ranks time. Inputs are resident in HBM before timing starts.
-* roofline: algorithmic bytes per launch = E * (54*U + 61) x steps per launch,
-  over the launch's average duration from HIP events on the stream the kernel runs on
-  (around every launch; for one-step launches around every chunk of 20, gaps included).
+* roofline: algorithmic bytes per launch over the launch's average duration from HIP events
+  on the stream the kernel runs on (around every launch; for one-step launches around every
+  chunk of 20, gaps included). One-step launch: E * (54*U + 61) (SURVEY.md 8d canonical:
+  state r+w 34 B/UE + outputs 20 B/UE; per env 61 B). Rollout launch of n steps: the outputs
+  of every step, E * n * (20*U + 5), plus the state read and written once, E * (34*U + 56).
   traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
-  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null --
-  below the algorithmic bytes because the state is 8 B per UE (canonical: 34 B) and, fused,
-  makes one round trip per launch instead of one per step.
+  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
   per core, run before the GPU is touched.
@@ -47,6 +49,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def algorithmic_bytes_per_env_step(num_ues: int, per_env_bs: bool, num_bs: int) -> int:
     # SURVEY.md 8d canonical layout: per UE 34 B state r+w + 20 B outputs; per env 61 B
     return 54 * num_ues + 61 + (8 * num_bs if per_env_bs else 0)
+
+
+def algorithmic_bytes_rollout(num_ues: int, per_env_bs: bool, num_bs: int, n: int) -> int:
+    """Per env, one rollout launch of n steps: every step's outputs (obs 16 B + serving 4 B
+    per UE, reward 4 + done 1 per env; per-env layouts: 8 B per station per step) plus the
+    canonical state read and written once (34 B per UE; PCG64 state r+w 32, inc 16, t r+w 8)."""
+    per_step = 20 * num_ues + 5 + (8 * num_bs if per_env_bs else 0)
+    return n * per_step + 34 * num_ues + 56
 
 
 # ---------------------------------------------------------------------------------------------
@@ -109,8 +119,9 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--launch", default="fused", choices=("fused", "single", "split"),
-                    help="fused: 20 steps per launch (default); single: one launch per step; "
-                         "split: one launch per step on two HIP streams (two env halves)")
+                    help="fused: one rollout launch of 20 steps, every step's outputs kept "
+                         "(default); single: one launch per step; split: one launch per step "
+                         "on two HIP streams (two env halves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
@@ -156,16 +167,25 @@ def main():
     per_env_bs = env.engine.bs_per_env
     parts = env.engine.launch_parts
     env.reset()
-    CHUNK = 20  # steps per engine.step call (one episode)
+    CHUNK = 20  # steps per engine call (one episode)
+    fused = args.launch == "fused" and env.engine.fused_steps
+    traj = env.engine.trajectory(CHUNK) if args.launch == "fused" else None
+
+    def chunk():
+        if traj is not None:
+            env.engine.rollout(CHUNK, traj)  # every step's outputs to its own row
+        else:
+            env.engine.step(CHUNK)
+
     # warmup (also brings the GPU to its steady clock): the Gym step once, then chunks
     if args.warmup > 0:
         env.step()
         for _ in range(-(-(args.warmup - 1) // CHUNK)):
-            env.engine.step(CHUNK)
+            chunk()
     torch.cuda.synchronize(device)
 
-    # Steps are issued in chunks of CHUNK from C (fused: one launch per chunk; single: CHUNK
-    # back-to-back launches -- a Python call per step would make the host the bottleneck),
+    # Steps are issued in chunks of CHUNK from C (fused: one rollout launch per chunk; single:
+    # CHUNK back-to-back launches -- a Python call per step would make the host the bottleneck),
     # with a HIP event pair around every chunk on the caller's stream. With the two-half
     # launch shape the second half runs on the context's own stream and is joined back
     # before mev_step returns, so each event pair brackets whole steps of the full batch.
@@ -179,7 +199,7 @@ def main():
     t0 = time.perf_counter()
     for a, b in ev:
         a.record(stream)
-        env.engine.step(CHUNK)
+        chunk()
         b.record(stream)
     if world > 1:  # the one collective: final (reward, done) batch to every rank
         gather_final(env.engine.reward, env.engine.done)
@@ -197,10 +217,9 @@ def main():
 
     if rank == 0:
         value = world * E * K / elapsed
-        bpe = algorithmic_bytes_per_env_step(U, per_env_bs, B)
-        fused = args.launch == "fused" and env.engine.fused_steps
         spl = CHUNK if fused else 1  # steps per launch
-        algo_bytes = E * bpe * spl
+        algo_bytes = E * (algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused else
+                          algorithmic_bytes_per_env_step(U, per_env_bs, B))
         launch_ms = kern_ms * spl
         achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
         traffic, rocprof_ms = load_profile(args.workload, E, args.launch)
@@ -230,8 +249,9 @@ def main():
                          "launch_ms": launch_ms,
                          "rocprof_launch_ms": rocprof_ms,
                          "launch_shape": (
-                             f"fused: {spl} steps per launch, env state in registers between "
-                             f"them, outputs written every step" if fused else
+                             f"fused rollout: {spl} steps per launch, env state in registers "
+                             f"between them, every step's outputs to its own trajectory row"
+                             if fused else
                              f"{parts} halves per step on {parts} HIP streams" if parts > 1
                              else "one kernel per step")},
             "cpu_baseline": cpu,

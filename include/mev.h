@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 6
+#define MEV_ABI_VERSION 7
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -168,14 +168,21 @@ int mev_prepare_draws(const mev_ctx* ctx, const mev_state* state, const uint8_t*
  * shared layout between resets. No-op for per-env layouts. Stream-ordered. */
 int mev_update_stations(const mev_ctx* ctx, const int32_t* bs_xy, void* stream);
 
-/* Advance every env by `nsteps` steps of MComCore.step (base.py:230-296), one
- * fused kernel launch per step. An env whose episode is over (t >= min(EP_MAX_TIME,
- * departure)) is reset at the start of its next step (lazy auto-reset), so a
- * sequence of steps reproduces the reference driver loop
- * `reset(); step() x20; reset(); ...` (collectData2.ipynb cells 3-4). Outputs hold
- * the last step's results. */
+/* Advance every env by `nsteps` steps of MComCore.step (base.py:230-296). An env whose
+ * episode is over (t >= min(EP_MAX_TIME, departure)) is reset at the start of its next step
+ * (lazy auto-reset), so a sequence of steps reproduces the reference driver loop
+ * `reset(); step() x20; reset(); ...` (collectData2.ipynb cells 3-4). nsteps > 1 with U <= 64
+ * runs as ONE launch (fuse_steps). Outputs hold the last step's results. */
 int mev_step(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
              int32_t nsteps, void* stream);
+
+/* mev_step keeping every step's outputs (one episode of the collectData2.ipynb loop, whose
+ * per-step dump base.py:261,298-349 consumes each step): the buffers of `traj` hold nsteps
+ * rows -- obs [n][E][U][4], serving [n][E][U], reward [n][E], done [n][E], rate64 / util64
+ * [n][E][U], metrics [n][E][4] -- and step i writes row i. qoe_stats stays [E][4]
+ * (per-episode, accumulated as in mev_step). Same results as nsteps mev_step calls. */
+int mev_rollout(const mev_ctx* ctx, const mev_state* st, const mev_outputs* traj,
+                int32_t nsteps, void* stream);
 
 /* Error text for a return code; last HIP error string for MEV_EHIP. */
 const char* mev_strerror(int code);

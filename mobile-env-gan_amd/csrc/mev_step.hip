@@ -92,6 +92,20 @@ struct KOut {
   double4* qoe_stats;  // [E] {count, sum, sum of squares, count below qoe_low}
 };
 
+// Outputs of row i of a trajectory (mev_rollout): every per-step output holds one row per
+// step; qoe_stats is per episode and not shifted.
+__host__ __device__ __forceinline__ KOut out_row(KOut o, int E, int U, int i) {
+  const size_t eu = (size_t)E * U * i, ee = (size_t)E * i;
+  o.obs += eu;
+  o.serving += eu;
+  o.reward += ee;
+  o.done += ee;
+  if (o.rate64) o.rate64 += eu;
+  if (o.util64) o.util64 += eu;
+  if (o.metrics) o.metrics += ee;
+  return o;
+}
+
 struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
@@ -418,6 +432,63 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
   }
 }
 
+// Outputs of one fused step held back until the next step's association gather is issued
+// (k_steps_packed): the global stores of step i then come after that load in program order,
+// so waiting for the gather (vmcnt counts loads and stores in issue order) does not also wait
+// for step i's stores to be acknowledged -- with trajectory rows every store allocates a new
+// L2 line and that wait is long.
+struct Pending {
+  int srv;
+  float4 obs;
+  double rate, util;
+  float reward;
+  float4 met;
+  uint32_t ui;
+  int e;
+  bool valid, lead, done;
+};
+
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+// s_waitcnt vmcnt(0) only (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait on those)
+__device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
+// The stores of a Pending step into row `row` of the output buffers (row 0 and nrows 1 when
+// the outputs are overwritten every step), branch-free: raw buffer stores over the whole
+// trajectory (loop-invariant descriptors; nrows * row bytes < 2^32, checked by the host) whose
+// lanes without data (padding lanes; non-leaders for the per-env rows) take the offset one
+// past the end, which the buffer range check drops. Without branches every path issues the
+// same VMEM ops, so the compiler's wait for the next gather can leave these stores in flight.
+template <bool LEAN>
+__device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p, uint32_t E,
+                                              uint32_t EU, uint32_t row, uint32_t nrows) {
+  const uint32_t robs = 16u * EU, rsrv = 4u * EU, rrew = 4u * E;  // row bytes
+  const uint32_t nobs = nrows * robs, nsrv = nrows * rsrv, nrew = nrows * rrew,
+                 ndone = nrows * E;
+  const v4u32 ob = {__float_as_uint(p.obs.x), __float_as_uint(p.obs.y),
+                    __float_as_uint(p.obs.z), __float_as_uint(p.obs.w)};
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving, nsrv),
+                                        p.valid ? row * rsrv + 4u * p.ui : nsrv, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
+                                         p.valid ? row * robs + 16u * p.ui : nobs, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
+                                        p.lead ? row * rrew + 4u * (uint32_t)p.e : nrew, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
+                                       p.lead ? row * E + (uint32_t)p.e : ndone, 0, 0);
+  if (!LEAN) {
+    const KOut o = out_row(out, (int)E, (int)(EU / E), (int)row);
+    if (p.valid) {
+      if (o.rate64) o.rate64[p.ui] = p.rate;
+      if (o.util64) o.util64[p.ui] = p.util;
+    }
+    if (p.lead && o.metrics) o.metrics[p.e] = p.met;
+  }
+}
+
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
 //   UC:   U as a compile-time constant (0: runtime kp.U) -- folds the lane map, the segment
 //         reductions and the env indexing for the registered scenario sizes;
@@ -426,12 +497,17 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
 //   FUSED: one of several steps of a launch (mev_step(n), n > 1): the env state stays in
 //         registers between the steps (`cur` is updated; the caller stores it after the last
 //         step), the per-step outputs are written every step as in separate launches.
+//   FUSED steps defer their output stores (Pending): `pend` holds the previous step's
+//   outputs (for row prev_row of nrows; nothing valid before the first step) and receives
+//   this step's. `out` is then the base (row 0) of the buffers.
 template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
                                              bool env_ok, int* __restrict__ hist,
-                                             const int* __restrict__ ltab = nullptr) {
+                                             const int* __restrict__ ltab = nullptr,
+                                             Pending* pend = nullptr, int prev_row = 0,
+                                             int nrows = 1) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   const int U = UC ? UC : kp.U;
@@ -484,6 +560,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       koff = 2 * U;
       wp = make_int2(-1, -1);
     }
+    if (FUSED) wait_vmem();  // see below
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
@@ -536,6 +613,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         if (need)
           s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
       }
+      // fused: the loads of this rare path land here, so the compiler's merged wait state
+      // after it has nothing pending from them (it would otherwise wait, on the common path
+      // too, for every store still in flight)
+      if (FUSED) wait_vmem();
     }
   }
   // owner of the env's new stream state: the last drawing lane, else (reset without draws)
@@ -597,6 +678,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       full = __hiloint2double(r.w, r.z);
     }
   }
+  // the previous fused step's stores, after this step's gather
+  if (FUSED)
+    flush_pending<LEAN>(out, *pend, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)prev_row,
+                        (uint32_t)nrows);
 
   // ---- 3. n_b of the own serving BS ---------------------------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
@@ -650,34 +735,41 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 6. stores ----------------------------------------------------------------------
-  if (valid) {
+  const float4 obs = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
+                                 (float)cents * 0.01f, (float)util);
+  const double util_out = active ? util : __builtin_nan("");
+  if (valid && !FUSED) {
     const uint32_t ui = (uint32_t)idx;
-    if (!FUSED) store_ue(&at(st.ue_state, 8u * ui), pos, wp);
+    store_ue(&at(st.ue_state, 8u * ui), pos, wp);
     at(out.serving, 4u * ui) = srv;
-    at(out.obs, 16u * ui) = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
-                                        (float)cents * 0.01f, (float)util);
-    if (!FUSED && own_fin)  // the stream moved (draws, or reset): write the new state back
+    at(out.obs, 16u * ui) = obs;
+    if (own_fin)  // the stream moved (draws, or reset): write the new state back
       at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) =
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
-    if (!LEAN && out.util64) out.util64[idx] = active ? util : __builtin_nan("");
+    if (!LEAN && out.util64) out.util64[idx] = util_out;
   }
-  if (env_ok && leader) {
+  const bool lead = env_ok && leader;
+  float reward_out = 0.f;
+  float4 met = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lead) {
     // np.mean; the lean path divides in float32 (the reward output is float32)
     const double mean_u =
         LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
                          : kp.lower)
              : (nact > 0 ? sum_u / (double)nact : kp.lower);
-    if (!FUSED) {
-      at(st.t, 4u * (uint32_t)e) = t + 1;
-      if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
-    }
-    at(out.reward, 4u * (uint32_t)e) = (float)mean_u;
-    at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
+    reward_out = (float)mean_u;
     if (want_metrics) {
       const int ncon = __popcll(mcon);
       const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
-      out.metrics[e] = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
+      met = make_float4((float)ncon, (float)ncon, (float)mean_u, (float)mean_r);
+    }
+    if (!FUSED) {
+      at(st.t, 4u * (uint32_t)e) = t + 1;
+      if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
+      at(out.reward, 4u * (uint32_t)e) = reward_out;
+      at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
+      if (want_metrics) out.metrics[e] = met;
     }
     if (want_qoe) {
       double4 a = t == 0 ? make_double4(0.0, 0.0, 0.0, 0.0) : out.qoe_stats[e];
@@ -687,6 +779,19 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       a.w += (double)nlow;
       out.qoe_stats[e] = a;
     }
+  }
+  if (FUSED) {  // held back until the next step's gather (or the end of the launch)
+    pend->srv = srv;
+    pend->obs = obs;
+    pend->rate = rate;
+    pend->util = util_out;
+    pend->reward = reward_out;
+    pend->met = met;
+    pend->ui = (uint32_t)idx;
+    pend->e = e;
+    pend->valid = valid;
+    pend->lead = lead;
+    pend->done = t + 1 >= kp.t_end;
   }
   if (FUSED) {
     cur.t = t + 1;
@@ -733,14 +838,15 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
                                             lds_hist + (threadIdx.x >> 6) * G * kp.B);
 }
 
-// nsteps fused steps per launch (mev_step(n), n > 1): each wavefront advances its env group
-// n steps with the state in registers -- loaded once, stored once -- and writes the step
-// outputs of every step (as n launches would; the caller sees the last step's). One launch
+// nsteps fused steps per launch (mev_step / mev_rollout with n > 1): each wavefront advances
+// its env group n steps with the state in registers -- loaded once, stored once -- and writes
+// the outputs of every step: into row i of the trajectory buffers (traj != 0, mev_rollout),
+// or over the previous step's (mev_step; the caller sees the last step's, as with n launches). One launch
 // instead of n removes n - 1 kernel boundaries and the fill / drain of every launch.
 template <bool PER_ENV_BS, bool LEAN, int UC>
 __global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KState st, KOut out,
                                                               KTables tb, int ngroups,
-                                                              int nsteps) {
+                                                              int nsteps, int traj) {
   extern __shared__ int lds_hist[];
   const int lane = threadIdx.x & 63;
   const int g = block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
@@ -767,9 +873,22 @@ __global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KStat
   }
   GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
   bool moved = false;
+  Pending pend;  // nothing to store before the first step
+  pend.valid = pend.lead = pend.done = false;
+  pend.srv = pend.ui = pend.e = 0;
+  pend.obs = pend.met = make_float4(0.f, 0.f, 0.f, 0.f);
+  pend.rate = pend.util = 0.0;
+  pend.reward = 0.f;
+  // the group's inputs have landed before the loop: otherwise the compiler's wait for them,
+  // merged into the loop header, would also wait for the previous step's stores
+  __builtin_amdgcn_s_waitcnt(0);
+  const int nrows = traj ? nsteps : 1;
   for (int i = 0; i < nsteps; ++i)
     moved |= packed_group<PER_ENV_BS, LEAN, UC, true>(kp, st, out, tb, m, a, e, env_ok, hist,
-                                                      ltab);
+                                                      ltab, &pend, traj ? max(i - 1, 0) : 0,
+                                                      nrows);
+  flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
+                      traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
   // the state after the last step
   if (env_ok && m.u < U)
     store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
@@ -1445,7 +1564,7 @@ static StepKernel step_kernel_for(bool per_env, bool lean, int U) {
   return lean ? step_kernel_u<false, true>(U) : step_kernel_u<false, false>(U);
 }
 
-typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int);
+typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
 
 template <bool PER_ENV_BS, bool LEAN>
 static StepsKernel steps_kernel_u(int U) {
@@ -1466,7 +1585,7 @@ static StepsKernel steps_kernel_for(bool per_env, bool lean, int U) {
 // the caller's stream, the second on c->aux (forked from and joined back into the caller's
 // stream); the halves are independent envs, so the two streams overlap freely.
 static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& ko,
-                               const KTables& tb, int nsteps, hipStream_t stream) {
+                               const KTables& tb, int nsteps, bool traj, hipStream_t stream) {
   const KParams& kp = c->kp;
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
@@ -1479,7 +1598,14 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     const size_t shmem_f =
         shmem + sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.tab_m;
-    kf<<<dim3(blocks), dim3(kPackedBlock), shmem_f, stream>>>(kp, ks, ko, tb, groups, nsteps);
+    // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^32 B)
+    const int64_t row_bytes = 16 * (int64_t)kp.E * kp.U;
+    const int rows_max = traj ? (int)std::max<int64_t>(1, 0xFFFFFFFFll / row_bytes) : nsteps;
+    for (int i0 = 0; i0 < nsteps; i0 += rows_max) {
+      const int n = std::min(rows_max, nsteps - i0);
+      kf<<<dim3(blocks), dim3(kPackedBlock), shmem_f, stream>>>(
+          kp, ks, traj ? out_row(ko, kp.E, kp.U, i0) : ko, tb, groups, n, traj ? 1 : 0);
+    }
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }
@@ -1488,7 +1614,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   if (c->parts == 1 || half <= 0 || half >= groups) {
     const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     for (int i = 0; i < nsteps; ++i)
-      k<<<dim3(blocks), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, 0, groups);
+      k<<<dim3(blocks), dim3(kPackedBlock), shmem, stream>>>(
+          kp, ks, traj ? out_row(ko, kp.E, kp.U, i) : ko, tb, 0, groups);
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }
@@ -1497,8 +1624,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   MEV_HIP(hipEventRecord(c->ev_fork, stream));
   MEV_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   for (int i = 0; i < nsteps; ++i) {
-    k<<<dim3(blocks0), dim3(kPackedBlock), shmem, stream>>>(kp, ks, ko, tb, 0, half);
-    k<<<dim3(blocks1), dim3(kPackedBlock), shmem, c->aux>>>(kp, ks, ko, tb, half, groups);
+    const KOut oi = traj ? out_row(ko, kp.E, kp.U, i) : ko;
+    k<<<dim3(blocks0), dim3(kPackedBlock), shmem, stream>>>(kp, ks, oi, tb, 0, half);
+    k<<<dim3(blocks1), dim3(kPackedBlock), shmem, c->aux>>>(kp, ks, oi, tb, half, groups);
   }
   MEV_HIP(hipGetLastError());
   MEV_HIP(hipEventRecord(c->ev_join, c->aux));
@@ -1522,7 +1650,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
       hipLaunchKernelGGL(k_reset_packed, grid, dim3(kPackedBlock), 0, stream, kp, ks, ko, tb,
                          mask);
     } else {
-      return launch_packed_steps(c, ks, ko, tb, 1, stream);
+      return launch_packed_steps(c, ks, ko, tb, 1, false, stream);
     }
   } else {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
@@ -1571,8 +1699,8 @@ int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   return launch<true>(c, st, out, env_mask, (hipStream_t)stream);
 }
 
-int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int32_t nsteps,
-             void* stream) {
+static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
+                     int32_t nsteps, bool traj, void* stream) {
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   if (nsteps < 0) return MEV_EINVAL;
@@ -1581,13 +1709,34 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
     KOut ko;
     to_kernel(st, out, ks, ko);
     const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn};
-    return launch_packed_steps(c, ks, ko, tb, nsteps, (hipStream_t)stream);
+    return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
   }
+  const int64_t eu = (int64_t)c->kp.E * c->kp.U, ee = c->kp.E;
   for (int i = 0; i < nsteps; ++i) {
-    rc = launch<false>(c, st, out, nullptr, (hipStream_t)stream);
+    mev_outputs oi = *out;
+    if (traj) {  // row i of the trajectory buffers (out_row)
+      oi.obs += 4 * eu * i;
+      oi.serving += eu * i;
+      oi.reward += ee * i;
+      oi.done += ee * i;
+      if (oi.rate64) oi.rate64 += eu * i;
+      if (oi.util64) oi.util64 += eu * i;
+      if (oi.metrics) oi.metrics += 4 * ee * i;
+    }
+    rc = launch<false>(c, st, &oi, nullptr, (hipStream_t)stream);
     if (rc) return rc;
   }
   return MEV_OK;
+}
+
+int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int32_t nsteps,
+             void* stream) {
+  return run_steps(c, st, out, nsteps, false, stream);
+}
+
+int mev_rollout(const mev_ctx* c, const mev_state* st, const mev_outputs* traj,
+                int32_t nsteps, void* stream) {
+  return run_steps(c, st, traj, nsteps, true, stream);
 }
 
 // --------------------------------------------------------------------------------------

@@ -80,6 +80,28 @@ class EngineParams:
         return min(int(self.ep_max_time), int(self.arrival_exit))
 
 
+@dataclass
+class Trajectory:
+    """Per-step outputs of a rollout, leading axis = step: obs [n,E,U,4] f32, serving [n,E,U]
+    i32, reward [n,E] f32, done [n,E] u8, and optionally rate64/util64 [n,E,U] f64,
+    metrics [n,E,4] f32."""
+    obs: torch.Tensor
+    serving: torch.Tensor
+    reward: torch.Tensor
+    done: torch.Tensor
+    rate64: "torch.Tensor | None" = None
+    util64: "torch.Tensor | None" = None
+    metrics: "torch.Tensor | None" = None
+
+    def rows(self, start: int, n: int) -> "Trajectory":
+        """Rows [start, start + n) as a trajectory (views; for rollouts of n steps that fill a
+        longer trajectory piece by piece)."""
+        def v(t):
+            return None if t is None else t[start:start + n]
+        return Trajectory(v(self.obs), v(self.serving), v(self.reward), v(self.done),
+                          v(self.rate64), v(self.util64), v(self.metrics))
+
+
 def _check_station_range(bs, bs_count=None):
     """Station coordinates must lie in [0, 1024) (mev.h: the association keys are 32-bit);
     per-env layouts with a station count: only the first bs_count[e] rows are stations."""
@@ -249,6 +271,48 @@ class StepEngine:
         with torch.cuda.device(self.device):
             N.check(self._lib.mev_step(self._ctx, C.byref(self._st), C.byref(self._out),
                                        int(nsteps), self._stream()), "mev_step")
+
+    def trajectory(self, nsteps: int) -> "Trajectory":
+        """Allocate trajectory buffers for rollout(nsteps): every per-step output with a
+        leading step axis (the optional float64 / metrics outputs as the engine was built)."""
+        E, U = self.p.num_envs, self.p.num_ues
+        kw = dict(device=self.device)
+        n = int(nsteps)
+        return Trajectory(
+            obs=torch.empty((n, E, U, 4), dtype=torch.float32, **kw),
+            serving=torch.empty((n, E, U), dtype=torch.int32, **kw),
+            reward=torch.empty((n, E), dtype=torch.float32, **kw),
+            done=torch.empty((n, E), dtype=torch.uint8, **kw),
+            rate64=(torch.empty((n, E, U), dtype=torch.float64, **kw)
+                    if self.rate64 is not None else None),
+            util64=(torch.empty((n, E, U), dtype=torch.float64, **kw)
+                    if self.util64 is not None else None),
+            metrics=(torch.empty((n, E, 4), dtype=torch.float32, **kw)
+                     if self.metrics is not None else None))
+
+    def rollout(self, nsteps: int, traj: "Trajectory | None" = None) -> "Trajectory":
+        """mev_rollout: ``nsteps`` steps (as step(nsteps): one launch for U <= 64) keeping
+        every step's outputs -- row i of the returned trajectory is step i. ``traj`` (from
+        trajectory(n), n >= nsteps) is reused when given. The engine's own one-step output
+        tensors (obs, serving, ...) are not written; qoe_stats accumulates as in step()."""
+        n = int(nsteps)
+        if traj is None:
+            traj = self.trajectory(n)
+        if traj.obs.shape[0] < n or tuple(traj.obs.shape[1:]) != tuple(self.obs.shape):
+            raise ValueError("trajectory buffers do not fit this engine / nsteps")
+        if (traj.rate64 is None) != (self.rate64 is None) or \
+                (traj.util64 is None) != (self.util64 is None) or \
+                (traj.metrics is None) != (self.metrics is None):
+            raise ValueError("trajectory outputs differ from the engine's output set")
+        if n == 0:
+            return traj
+        out = N.MevOutputs(_ptr(traj.obs), _ptr(traj.serving), _ptr(traj.reward),
+                           _ptr(traj.done), _ptr(traj.rate64), _ptr(traj.util64),
+                           _ptr(traj.metrics), _ptr(self.qoe_stats))
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_rollout(self._ctx, C.byref(self._st), C.byref(out), n,
+                                          self._stream()), "mev_rollout")
+        return traj
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and self._ctx.value:

@@ -40,7 +40,8 @@ def make_oracle(d, bs=None, ue=None):
     return OracleBatch(p, bs_xy, d["xy"].shape[2], d["seeds"], bs_count=cnt)
 
 
-def make_engine(d, device="cuda", bs=None, ue=None, stream_split=0, draw_table=-1, **kw):
+def make_engine(d, device="cuda", bs=None, ue=None, stream_split=0, draw_table=-1, fuse_steps=0,
+                **kw):
     from mobile_env.core.engine import EngineParams, StepEngine
     bs_xy, cnt = layout_for(d)
     E = len(d["seeds"])
@@ -48,5 +49,6 @@ def make_engine(d, device="cuda", bs=None, ue=None, stream_split=0, draw_table=-
     B = bs_xy.shape[-2]
     p = EngineParams(num_envs=E, num_ues=U, num_bs=B, velocity=float(d["velocity"]),
                      bs=dict(bs or DEFAULT_BS), ue=dict(ue or DEFAULT_UE),
-                     stream_split=stream_split, draw_table=draw_table)
+                     stream_split=stream_split, draw_table=draw_table,
+                     fuse_steps=fuse_steps)
     return StepEngine(p, bs_xy, d["seeds"], bs_count=cnt, device=device, **kw)
