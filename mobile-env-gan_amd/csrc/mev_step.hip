@@ -32,7 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
+#include <vector>
 
 #include "mev.h"
 
@@ -69,6 +71,9 @@ struct KParams {
   int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
   float vel_f;
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
+  // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
+  int lds_assoc;      // bytes of the blob (multiple of 16)
+  int lds_st_off, lds_rank_off, lds_rate_off;  // byte offsets of its parts
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
 };
@@ -117,6 +122,15 @@ struct KTables {
   const int* tab_xy;        // [E][M] int16x2
   const u128* tab_st;       // [E][M]
   int* drawn;               // [E]
+  // Compact form of `assoc` that fits in LDS (copied once per workgroup by the fused launch):
+  //   [0, lds_st_off)          serving station per grid cell, 4 bits (15 = none), 2 per byte
+  //   [lds_st_off, +64)        station coordinates x | y << 16 (16 slots)
+  //   [lds_rank_off, ...)      uint2 {bits, prefix} per 32 squared distances: bit d of the
+  //                            set S of sums of two squares <= d2max, prefix = |S below word|
+  //   [lds_rate_off, ...)      rate_full[d] for d in S, in increasing d (rank of d in S)
+  // so full = rate[rank(d2)] with d2 to the serving station: the same float64 values as
+  // `assoc`, from four LDS reads instead of one 16-byte gather from L2 per UE and step.
+  const int4* lds_blob;
 };
 
 // Element at a 32-bit byte offset from a wave-uniform base: addresses become
@@ -274,6 +288,16 @@ __device__ __forceinline__ double utility_of(double rate, double cents, const KP
 
 constexpr int kPackedBlock = 256;
 constexpr int kWavesPerBlock = kPackedBlock / 64;
+// fused launches with the LDS association tables: 10-wave workgroups, two per CU (one LDS copy
+// of the <= ~65 KB tables per 10 waves; 5 waves per SIMD, the kernel's register limit)
+#ifndef MEV_LDS_WAVES
+#define MEV_LDS_WAVES 8
+#endif
+constexpr int kLdsWaves = MEV_LDS_WAVES;
+constexpr int kLdsBytesPerWG = 80 * 1024;
+#ifndef MEV_STORE_AUX
+#define MEV_STORE_AUX 0  // cache policy of the fused steps' output stores
+#endif
 
 
 // Sum of `v` over the lanes of one env segment that have `take` set (segment = lanes
@@ -384,8 +408,8 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   g.s_ok = true;
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue(&at(st.ue_state, 8u * ue));
-  if (kp.tab_m && !fused) {  // the stream state is read only when a draw falls beyond the table
-    g.drawn = at(tb.drawn, 4u * (uint32_t)ec);
+  if (fused || kp.tab_m) {  // the stream state is read only where a draw needs it (fused:
+    g.drawn = kp.tab_m ? at(tb.drawn, 4u * (uint32_t)ec) : 0;  // the caller's LDS slot)
     g.pa = g.pb = make_ulonglong2(0, 0);
   } else {
     ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
@@ -453,6 +477,17 @@ typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 // s_waitcnt vmcnt(0) only (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait on those)
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// LDS-DMA: this lane's element `src` to lds_base + lane * sizeof(T) (lds_base wave-uniform);
+// complete after vmcnt(0)
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+__device__ __forceinline__ void glds(const int* src, int* lds_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_base, 4, 0, 0);
+}
+__device__ __forceinline__ void glds(const int4* src, int4* lds_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_base, 16, 0, 0);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
@@ -472,13 +507,13 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
   const v4u32 ob = {__float_as_uint(p.obs.x), __float_as_uint(p.obs.y),
                     __float_as_uint(p.obs.z), __float_as_uint(p.obs.w)};
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving, nsrv),
-                                        p.valid ? row * rsrv + 4u * p.ui : nsrv, 0, 0);
+                                        p.valid ? row * rsrv + 4u * p.ui : nsrv, 0, MEV_STORE_AUX);
   __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
-                                         p.valid ? row * robs + 16u * p.ui : nobs, 0, 0);
+                                         p.valid ? row * robs + 16u * p.ui : nobs, 0, MEV_STORE_AUX);
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
-                                        p.lead ? row * rrew + 4u * (uint32_t)p.e : nrew, 0, 0);
+                                        p.lead ? row * rrew + 4u * (uint32_t)p.e : nrew, 0, MEV_STORE_AUX);
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
-                                       p.lead ? row * E + (uint32_t)p.e : ndone, 0, 0);
+                                       p.lead ? row * E + (uint32_t)p.e : ndone, 0, MEV_STORE_AUX);
   if (!LEAN) {
     const KOut o = out_row(out, (int)E, (int)(EU / E), (int)row);
     if (p.valid) {
@@ -500,14 +535,18 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //   FUSED steps defer their output stores (Pending): `pend` holds the previous step's
 //   outputs (for row prev_row of nrows; nothing valid before the first step) and receives
 //   this step's. `out` is then the base (row 0) of the buffers.
-template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED>
+//   LDSA: (fused, shared layout) association from the LDS copy of the compact tables at
+//         `lblob` (KTables::lds_blob) instead of the L2 gather.
+template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, bool LDSA = false>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
                                              bool env_ok, int* __restrict__ hist,
                                              const int* __restrict__ ltab = nullptr,
                                              Pending* pend = nullptr, int prev_row = 0,
-                                             int nrows = 1) {
+                                             int nrows = 1,
+                                             const char* __restrict__ lblob = nullptr,
+                                             u128* __restrict__ lpcg = nullptr) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   const int U = UC ? UC : kp.U;
@@ -524,8 +563,11 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   int t = cur.t;
   int2 pos = make_int2(cur.s.x, cur.s.y);
   int2 wp = make_int2(cur.s.z, cur.s.w);
-  u128 inc = mk128(cur.pb.x, cur.pb.y);
-  u128 s = mk128(cur.pa.x, cur.pa.y);
+  // fused: the env's stream {state, increment} lives in the wavefront's LDS slot lpcg[seg]
+  // (read only where a draw needs it, written by the owner of a new state), not in registers
+  u128* const slot = FUSED ? lpcg + 2 * m.seg : nullptr;
+  u128 inc = FUSED ? (u128)0 : mk128(cur.pb.x, cur.pb.y);
+  u128 s = FUSED ? (u128)0 : mk128(cur.pa.x, cur.pa.y);
   const int M = kp.tab_m;  // wave-uniform
   int drawn = cur.drawn;
   bool s_ok = cur.s_ok;
@@ -555,12 +597,16 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       }
     } else if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc = at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e + 32u);
+      if (FUSED) {
+        inc = slot[1];
+        if (!kp.movement_reseed) s = slot[0];
+      }
       if (kp.movement_reseed) s = mk128(pc.x, pc.y);
       s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       koff = 2 * U;
       wp = make_int2(-1, -1);
+      if (FUSED) wait_vmem();  // in the loads' own block (see the fallback path below)
     }
-    if (FUSED) wait_vmem();  // see below
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
@@ -595,15 +641,25 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
           const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
           inc = mk128(pb.x, pb.y);
           s = mk128(pa.x, pa.y);
-        } else if (!s_ok && drawn > 0) {  // fused: the registers may trail the table draws
-          s = at(const_cast<u128*>(tb.tab_st),
-                 16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(min(drawn, M) - 1)));
+        } else {  // fused: the slot holds the state after a fallback draw, else the table
+          inc = slot[1];
+          if (!s_ok && drawn > 0) {
+            s = at(const_cast<u128*>(tb.tab_st),
+                   16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(min(drawn, M) - 1)));
+            wait_vmem();  // in the load's own block (see the wait below)
+          } else {
+            s = slot[0];
+          }
         }
         if (reset_env) {  // the state after this episode's U initial pairs
           const u128 su = at(const_cast<u128*>(tb.tab_st),
                              16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(U - 1)));
           s = su;
+          if (FUSED) wait_vmem();
         }
+      } else if (FUSED) {  // no table: the slot (after a reset this step: the reset's state)
+        inc = slot[1];
+        if (!do_reset) s = slot[0];
       }
       // common case: every drawing lane of the wave is the first of its env and no reset
       // came before -> two steps of the constant multiplier instead of a table jump
@@ -623,16 +679,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // the last UE's lane, else nobody (the stream did not move)
   const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
   if (FUSED) {
-    if (!M || fell_back) {  // every lane of an env whose stream moved takes the new state
-      const uint64_t mown = __ballot(own_fin);
-      if (mown) {
-        const uint64_t segown = mown & segmask;
-        const int src = segown ? 63 - __clzll((unsigned long long)segown) : __lane_id();
-        const u128 sb = shfl_u128(s_fin, src);
-        if (segown) s = sb;
-      }
-    }
-    if (M) {  // with the table, the registers hold the state only after a fallback draw
+    if ((!M || fell_back) && own_fin) slot[0] = s_fin;  // the env's new stream state
+    if (M) {  // with the table, the slot holds the state only after a fallback draw
       if (fell_back && tot > 0) s_ok = true;
       else if (tot > 0 || reset_env) s_ok = false;
     }
@@ -672,16 +720,40 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     // serving station (or -1) and the full rate of that pair -- one 16-byte gather from an
     // L2-resident table replaces the per-station loop and the rate-table read
     const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
-    const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));
-    if (active) {
-      srv = r.x;
-      full = __hiloint2double(r.w, r.z);
+    if (LDSA) {
+      // the same association from LDS: station of the cell (4 bits), d2 to it, and the full
+      // rate at the rank of d2 in the set of sums of two squares (KTables::lds_blob)
+      const uint32_t cell = (uint32_t)(yi * kp.W + xi);
+      const uint32_t nib =
+          ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
+          15u;
+      if (active && nib != 15u) {
+        srv = (int)nib;
+        const int sp = *reinterpret_cast<const int*>(lblob + kp.lds_st_off + 4u * nib);
+        const int dx = pos.x - (int)(short)sp, dy = pos.y - (sp >> 16);
+        const uint32_t d2 = (uint32_t)(dx * dx + dy * dy);
+        const uint2 w = *reinterpret_cast<const uint2*>(lblob + kp.lds_rank_off + 8u * (d2 >> 5));
+        const uint32_t k = w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
+        full = *reinterpret_cast<const double*>(lblob + kp.lds_rate_off + 8u * k);
+      }
+    } else {
+      const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));
+      if (active) {
+        srv = r.x;
+        full = __hiloint2double(r.w, r.z);
+      }
     }
   }
-  // the previous fused step's stores, after this step's gather
-  if (FUSED)
+  // the previous fused step's stores, after this step's gather; then the gather is waited for
+  // on every path (an empty asm reading its registers): a lane or wave that never reads
+  // `full` (no server) would otherwise carry the load as pending around the loop, and the
+  // compiler's merged wait before its register is reused is vmcnt(0) -- which also waits for
+  // every store just issued
+  if (FUSED) {
     flush_pending<LEAN>(out, *pend, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)prev_row,
                         (uint32_t)nrows);
+    asm volatile("" ::"v"(srv), "v"(full));
+  }
 
   // ---- 3. n_b of the own serving BS ---------------------------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
@@ -798,8 +870,6 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cur.s = make_int4(pos.x, pos.y, wp.x, wp.y);
     cur.drawn = drawn + tot;
     cur.s_ok = s_ok;
-    cur.pa = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
-    cur.pb = make_ulonglong2((uint64_t)inc, (uint64_t)(inc >> 64));
   }
   return __ballot(own_fin) & segmask;  // the env's stream moved this step
 }
@@ -843,66 +913,98 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
 // the outputs of every step: into row i of the trajectory buffers (traj != 0, mev_rollout),
 // or over the previous step's (mev_step; the caller sees the last step's, as with n launches). One launch
 // instead of n removes n - 1 kernel boundaries and the fill / drain of every launch.
-template <bool PER_ENV_BS, bool LEAN, int UC>
-__global__ __launch_bounds__(kPackedBlock) void k_steps_packed(KParams kp, KState st, KOut out,
-                                                              KTables tb, int ngroups,
-                                                              int nsteps, int traj) {
-  extern __shared__ int lds_hist[];
+//   LDSA: workgroups of kLdsWaves waves share one LDS copy of the compact association tables
+//   (shared layouts whose tables fit, KParams::lds_assoc), copied once; the grid is then sized
+//   to the resident workgroups (persistent: each wave takes groups g, g + T, g + 2T, ... of the
+//   T waves of the grid), so the copy is made once per workgroup slot, not once per group.
+template <bool PER_ENV_BS, bool LEAN, int UC, bool LDSA>
+__global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_packed(
+    KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj) {
+  extern __shared__ int lds_all[];
+  constexpr int NW = LDSA ? kLdsWaves : kWavesPerBlock;  // waves per workgroup
+  int* lds_hist = lds_all;
+  const char* lblob = nullptr;
+  if (LDSA) {
+    // LDS-DMA copy (no registers): wave w moves 1 KB pieces w, w + NW, ...
+    const int n16 = kp.lds_assoc >> 4;
+    const int ln = threadIdx.x & 63;
+    for (int c = (int)(threadIdx.x >> 6); c * 64 < n16; c += NW)
+      if (c * 64 + ln < n16) glds(tb.lds_blob + c * 64 + ln, reinterpret_cast<int4*>(lds_all) + c * 64);
+    wait_vmem();
+    __syncthreads();
+    lblob = reinterpret_cast<const char*>(lds_all);
+    lds_hist = lds_all + (kp.lds_assoc >> 2);
+  }
   const int lane = threadIdx.x & 63;
-  const int g = block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= ngroups) return;
+  const int wv = threadIdx.x >> 6;
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;
   const int U = UC ? UC : kp.U;
   const int P = PC ? PC : kp.U;
   const int G = PC ? 64 / (PC ? PC : 1) : kp.envs_per_wave;
   const LaneMap m = lane_map<PC>(lane, P);
-  const int e = g * G + m.seg;
-  const bool env_ok = (m.seg < G) && (e < kp.E);
-  const int wv = threadIdx.x >> 6;
-  int* hist = lds_hist + wv * G * kp.B * kp.hist_lds;
-  // the group's episode draw tables (x, y pairs) in LDS for the whole launch
-  int* ltab = lds_hist + kWavesPerBlock * G * kp.B * kp.hist_lds + wv * G * kp.tab_m;
-  if (kp.tab_m) {
-    const int n = G * kp.tab_m;
-    const int* src = tb.tab_xy + (size_t)g * n;
-    const int lim = (kp.E - g * G) * kp.tab_m;  // rows of envs that exist
-    for (int i = lane; i < n; i += 64)
-      if (i < lim) ltab[i] = src[i];
-    __builtin_amdgcn_wave_barrier();
-  }
-  GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
-  bool moved = false;
-  Pending pend;  // nothing to store before the first step
-  pend.valid = pend.lead = pend.done = false;
-  pend.srv = pend.ui = pend.e = 0;
-  pend.obs = pend.met = make_float4(0.f, 0.f, 0.f, 0.f);
-  pend.rate = pend.util = 0.0;
-  pend.reward = 0.f;
-  // the group's inputs have landed before the loop: otherwise the compiler's wait for them,
-  // merged into the loop header, would also wait for the previous step's stores
-  __builtin_amdgcn_s_waitcnt(0);
-  const int nrows = traj ? nsteps : 1;
-  for (int i = 0; i < nsteps; ++i)
-    moved |= packed_group<PER_ENV_BS, LEAN, UC, true>(kp, st, out, tb, m, a, e, env_ok, hist,
-                                                      ltab, &pend, traj ? max(i - 1, 0) : 0,
-                                                      nrows);
-  flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
-                      traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
-  // the state after the last step
-  if (env_ok && m.u < U)
-    store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
-             make_int2(a.s.z, a.s.w));
-  const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
-  if (env_ok && leader) {
-    at(st.t, 4u * (uint32_t)e) = a.t;
-    if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
-    if (moved) {  // the state after the last pair drawn
-      const ulonglong2 sf =
-          a.s_ok ? a.pa
-                 : at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
-                      16u * ((uint32_t)e * (uint32_t)kp.tab_m + (uint32_t)(a.drawn - 1)));
-      at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) = sf;
+  // per wave: stream slots [G][2] u128 {state, inc}, the n_b histogram, the group's episode
+  // draw tables (x, y pairs) in LDS for the whole launch (lds_per_wave)
+  u128* lpcg = reinterpret_cast<u128*>(lds_hist) + wv * G * 2;
+  int* hist = lds_hist + NW * G * 8 + wv * G * kp.B * kp.hist_lds;
+  int* ltab = lds_hist + NW * G * 8 + NW * G * kp.B * kp.hist_lds + wv * G * kp.tab_m;
+  const int gstride = LDSA ? (int)gridDim.x * NW : ngroups;
+  for (int g = block_slot(kp.xcd_remap) * NW + wv; g < ngroups; g += gstride) {
+    const int e = g * G + m.seg;
+    const bool env_ok = (m.seg < G) && (e < kp.E);
+    if (kp.tab_m) {  // LDS-DMA copy, 256 B per instruction
+      const int n = G * kp.tab_m;
+      const int* src = tb.tab_xy + (size_t)g * n;
+      const int lim = min(n, (kp.E - g * G) * kp.tab_m);  // rows of envs that exist
+      for (int c = 0; c * 64 < lim; ++c)
+        if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
+      wait_vmem();
+      __builtin_amdgcn_wave_barrier();
+    }
+    GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
+    const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
+    if (env_ok && leader) {
+      ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+      const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
+      lpcg[2 * m.seg] = mk128(pa.x, pa.y);
+      lpcg[2 * m.seg + 1] = mk128(pb.x, pb.y);
+    }
+    bool moved = false;
+    Pending pend;  // nothing to store before the first step
+    pend.valid = pend.lead = pend.done = false;
+    pend.srv = pend.ui = pend.e = 0;
+    pend.obs = pend.met = make_float4(0.f, 0.f, 0.f, 0.f);
+    pend.rate = pend.util = 0.0;
+    pend.reward = 0.f;
+    // the group's inputs have landed before the loop: otherwise the compiler's wait for them,
+    // merged into the loop header, would also wait for the previous step's stores
+    __builtin_amdgcn_s_waitcnt(0);
+    const int nrows = traj ? nsteps : 1;
+    for (int i = 0; i < nsteps; ++i)
+      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSA>(
+          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? max(i - 1, 0) : 0, nrows,
+          lblob, lpcg);
+    flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
+                        traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
+    // the state after the last step
+    if (env_ok && m.u < U)
+      store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
+               make_int2(a.s.z, a.s.w));
+    if (env_ok && leader) {
+      at(st.t, 4u * (uint32_t)e) = a.t;
+      if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
+      if (moved) {  // the state after the last pair drawn
+        // (one global load from either the table entry or, without a table, the env's own
+        // state, selected by value: a select of addresses would put a.pa on the stack)
+        ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
+        const ulonglong2 tv =
+            kp.tab_m ? at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
+                          16u * ((uint32_t)e * (uint32_t)kp.tab_m + (uint32_t)max(a.drawn - 1, 0)))
+                     : at(pcg2, 48u * (uint32_t)e);
+        const u128 sl = lpcg[2 * m.seg];
+        const ulonglong2 sf = a.s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
+        at(pcg2, 48u * (uint32_t)e) = sf;
+      }
     }
   }
 }
@@ -1210,6 +1312,22 @@ __global__ void k_assoc_map(const int2* __restrict__ bs, int B, int W, int H, in
   map[i] = r;
 }
 
+// Compact association tables (KTables::lds_blob), layout part: the serving station of every
+// cell from the association map as 4 bits (15 = none), and the station coordinates. One thread
+// per byte of the cell map (two cells).
+__global__ void k_lds_map(const int2* __restrict__ bs, int B, int cells,
+                          const int4* __restrict__ map, uint8_t* __restrict__ blob, int st_off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 16) {
+    const int2 q = i < B ? bs[i] : make_int2(0, 0);
+    reinterpret_cast<int*>(blob + st_off)[i] = (int)(((unsigned)q.x & 0xffffu) | ((unsigned)q.y << 16));
+  }
+  if (2 * i >= cells) return;
+  const int s0 = map[2 * i].x;
+  const int s1 = 2 * i + 1 < cells ? map[2 * i + 1].x : -1;
+  blob[i] = (uint8_t)((s0 < 0 ? 15 : s0) | ((s1 < 0 ? 15 : s1) << 4));
+}
+
 // Episode draw table of the envs with mask[e] (all if NULL): pair k of env e = draws 2k and
 // 2k + 1 of the stream re-seeded to state0 (what every episode of the env draws, in order),
 // and the stream state after them. One thread per (env, pair).
@@ -1265,6 +1383,8 @@ struct mev_ctx {
   u128* jump;
   double* util;
   int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
+  int4* blob;     // its compact LDS form (KTables::lds_blob; null when it does not fit)
+  int lds_wgs;    // resident workgroups of the LDSA fused kernel (CUs x per CU)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
   int fuse_steps;     // mev_step(n > 1): one fused launch (params.fuse_steps)
   int* tab_xy;        // episode draw table (params.draw_table), see KTables
@@ -1314,6 +1434,85 @@ static int validate(const mev_params* p) {
   if ((int64_t)p->num_envs * p->num_ues >= ((int64_t)1 << 28)) return MEV_EINVAL;
   if (!(p->velocity >= 0.0) || !(p->ue_noise > 0.0) || !(p->util_upper > p->util_lower))
     return MEV_EINVAL;
+  return MEV_OK;
+}
+
+typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
+static StepsKernel steps_kernel_for(bool per_env, bool lean, bool ldsa, int U);
+
+// LDS per workgroup of the fused LDSA kernel beyond the tables: each wave's n_b histogram and
+// episode draw table.
+static size_t lds_per_wave(const KParams& kp) {
+  return sizeof(int) * (size_t)kp.envs_per_wave * (8 + (size_t)kp.B * kp.hist_lds + kp.tab_m);
+}
+
+// The layout-independent parts of the compact association tables (KTables::lds_blob): the
+// set S of sums of two squares <= d2max as a rank index, and rate_full over S. Every d2 of a
+// UE to a station is a sum of two squares, so rank(d2) indexes the compact rate array for every
+// connectable pair. The layout part (cell map, stations) is written by mev_update_stations.
+// Leaves c->blob null (the kernel then gathers from `assoc`) when the shape does not qualify:
+// per-env layouts, more than 15 stations, U > 64, or tables larger than one workgroup's share.
+static int build_lds_tables(mev_ctx* c) {
+  KParams& kp = c->kp;
+  kp.lds_assoc = 0;
+  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch
+  if ((sw && atoi(sw) == 0) || c->p.bs_per_env || kp.B > 15 || kp.U > 64) return MEV_OK;
+  const int cells = kp.W * kp.H;
+  const int d2max = c->d2max;
+  const size_t nwords = (size_t)d2max / 32 + 1;
+  std::vector<uint32_t> bits(nwords, 0u);
+  for (int a = 0; (int64_t)a * a <= d2max; ++a)
+    for (int b = a; (int64_t)a * a + (int64_t)b * b <= d2max; ++b) {
+      const int d = a * a + b * b;
+      bits[(size_t)d >> 5] |= 1u << (d & 31);
+    }
+  std::vector<uint32_t> rank(2 * nwords);
+  uint32_t count = 0;
+  for (size_t w = 0; w < nwords; ++w) {
+    rank[2 * w] = bits[w];
+    rank[2 * w + 1] = count;
+    count += (uint32_t)__builtin_popcount(bits[w]);
+  }
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t st_off = up16(((size_t)cells + 1) / 2);
+  const size_t rank_off = st_off + 64;
+  const size_t rate_off = up16(rank_off + 8 * nwords);
+  const size_t total = up16(rate_off + 8 * (size_t)count);
+  if (total + kLdsWaves * lds_per_wave(kp) > (size_t)kLdsBytesPerWG) return MEV_OK;
+  std::vector<double> full((size_t)d2max + 1);
+  MEV_HIP(hipMemcpy(full.data(), c->rate_full, sizeof(double) * full.size(),
+                    hipMemcpyDeviceToHost));
+  std::vector<char> host(total - st_off, 0);  // stations, rank, rates (cell map: device)
+  memcpy(host.data() + (rank_off - st_off), rank.data(), 8 * nwords);
+  double* rates = reinterpret_cast<double*>(host.data() + (rate_off - st_off));
+  for (int d = 0, k = 0; d <= d2max; ++d)
+    if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) rates[k++] = full[(size_t)d];
+  if (hipMalloc(&c->blob, total) != hipSuccess) return MEV_ENOMEM;
+  MEV_HIP(hipMemset(c->blob, 0xff, st_off));  // no station anywhere until a layout is set
+  MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + st_off, host.data(), host.size(),
+                    hipMemcpyHostToDevice));
+  kp.lds_assoc = (int)total;
+  kp.lds_st_off = (int)st_off;
+  kp.lds_rank_off = (int)rank_off;
+  kp.lds_rate_off = (int)rate_off;
+  // persistent grid: every resident workgroup (the fewer of the two output variants)
+  int cus = 0;
+  MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  const size_t shmem = total + kLdsWaves * lds_per_wave(kp);
+  int per = 1 << 30;
+  for (int lean = 0; lean < 2; ++lean) {
+    int n = 0;
+    MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void*>(steps_kernel_for(false, lean != 0, true, kp.U)),
+        64 * kLdsWaves, shmem));
+    per = std::min(per, n);
+  }
+  c->lds_wgs = cus * per;
+  if (c->lds_wgs <= 0) {  // cannot be resident: the L2 gather path
+    (void)hipFree(c->blob);
+    c->blob = nullptr;
+    kp.lds_assoc = 0;
+  }
   return MEV_OK;
 }
 
@@ -1454,6 +1653,11 @@ int mev_create(const mev_params* params, mev_ctx** out) {
       return MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(c->assoc, 0xff, bytes));  // srv -1 everywhere until a layout is set
+    rc = build_lds_tables(c);
+    if (rc) {
+      mev_destroy(c);
+      return rc;
+    }
   }
 
   // ---- utility table over rounded rates ----
@@ -1503,6 +1707,7 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
   if (c->assoc) (void)hipFree(c->assoc);
+  if (c->blob) (void)hipFree(c->blob);
   if (c->tab_xy) (void)hipFree(c->tab_xy);
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
@@ -1564,21 +1769,22 @@ static StepKernel step_kernel_for(bool per_env, bool lean, int U) {
   return lean ? step_kernel_u<false, true>(U) : step_kernel_u<false, false>(U);
 }
 
-typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
 
-template <bool PER_ENV_BS, bool LEAN>
+template <bool PER_ENV_BS, bool LEAN, bool LDSA>
 static StepsKernel steps_kernel_u(int U) {
   switch (U) {
-    case 5: return k_steps_packed<PER_ENV_BS, LEAN, 5>;
-    case 15: return k_steps_packed<PER_ENV_BS, LEAN, 15>;
-    case 30: return k_steps_packed<PER_ENV_BS, LEAN, 30>;
-    default: return k_steps_packed<PER_ENV_BS, LEAN, 0>;
+    case 5: return k_steps_packed<PER_ENV_BS, LEAN, 5, LDSA>;
+    case 15: return k_steps_packed<PER_ENV_BS, LEAN, 15, LDSA>;
+    case 30: return k_steps_packed<PER_ENV_BS, LEAN, 30, LDSA>;
+    default: return k_steps_packed<PER_ENV_BS, LEAN, 0, LDSA>;
   }
 }
 
-static StepsKernel steps_kernel_for(bool per_env, bool lean, int U) {
-  if (per_env) return lean ? steps_kernel_u<true, true>(U) : steps_kernel_u<true, false>(U);
-  return lean ? steps_kernel_u<false, true>(U) : steps_kernel_u<false, false>(U);
+static StepsKernel steps_kernel_for(bool per_env, bool lean, bool ldsa, int U) {
+  if (per_env)
+    return lean ? steps_kernel_u<true, true, false>(U) : steps_kernel_u<true, false, false>(U);
+  if (ldsa) return lean ? steps_kernel_u<false, true, true>(U) : steps_kernel_u<false, false, true>(U);
+  return lean ? steps_kernel_u<false, true, false>(U) : steps_kernel_u<false, false, false>(U);
 }
 
 // Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
@@ -1594,16 +1800,22 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;
   // n > 1 steps on one stream: one launch of the fused multi-step kernel
   if (nsteps > 1 && c->parts == 1 && c->fuse_steps) {
-    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
-    const int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t shmem_f =
-        shmem + sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.tab_m;
+    // LDS association tables for trajectory launches (measured at 65,536 mobile-large envs:
+    // 16.0 vs 19.3 us per step, where the L2 gather competes with the stream of trajectory
+    // stores); a launch that overwrites its outputs keeps the L2 gather (11.9 vs 15.1 us: the
+    // stores stay in L2 and the tables' LDS cost occupancy, 4 vs 5 waves per SIMD)
+    const bool ldsa = kp.lds_assoc > 0 && !c->p.bs_per_env && traj;
+    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsa, kp.U);
+    const int nw = ldsa ? kLdsWaves : kWavesPerBlock;
+    int blocks = (groups + nw - 1) / nw;
+    if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
+    const size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
     // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^32 B)
     const int64_t row_bytes = 16 * (int64_t)kp.E * kp.U;
     const int rows_max = traj ? (int)std::max<int64_t>(1, 0xFFFFFFFFll / row_bytes) : nsteps;
     for (int i0 = 0; i0 < nsteps; i0 += rows_max) {
       const int n = std::min(rows_max, nsteps - i0);
-      kf<<<dim3(blocks), dim3(kPackedBlock), shmem_f, stream>>>(
+      kf<<<dim3(blocks), dim3(64 * nw), shmem_f, stream>>>(
           kp, ks, traj ? out_row(ko, kp.E, kp.U, i0) : ko, tb, groups, n, traj ? 1 : 0);
     }
     MEV_HIP(hipGetLastError());
@@ -1640,7 +1852,8 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn};
+  KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
+             c->blob};
   const KParams& kp = c->kp;
   const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
@@ -1673,6 +1886,13 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                      reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
                      c->p.height, c->d2max, c->rate_full, c->assoc);
   MEV_HIP(hipGetLastError());
+  if (c->blob) {
+    const int bytes = (cells + 1) / 2;
+    hipLaunchKernelGGL(k_lds_map, dim3((bytes + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, cells, c->assoc,
+                       reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_st_off);
+    MEV_HIP(hipGetLastError());
+  }
   return MEV_OK;
 }
 
@@ -1708,7 +1928,8 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
     KState ks;
     KOut ko;
     to_kernel(st, out, ks, ko);
-    const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn};
+    const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
+                     c->blob};
     return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
   }
   const int64_t eu = (int64_t)c->kp.E * c->kp.U, ee = c->kp.E;

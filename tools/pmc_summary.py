@@ -64,7 +64,7 @@ def main():
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
         for row in rows_of(stats[0], "Name"):
             if kre.search(row["Name"]):
-                summary["kernel"] = row["Name"].split("(")[0]
+                summary["kernel"] = re.sub(r"\(\w+::KParams.*", "", row["Name"])
                 summary["stats_avg_ns"] = float(row["AverageNs"])
                 summary["stats_calls"] = int(row["Calls"])
 
@@ -103,9 +103,18 @@ def main():
         summary["hbm_bytes_per_step"] = (fetch + write) / steps_per_launch
         summary["fetch_bytes_per_launch_corrected"] = fetch
         summary["write_bytes_per_launch"] = write
-    if "SQ_INSTS_VALU" in pmc and pmc.get("SQ_WAVES"):
-        summary["valu_per_wave_per_step"] = pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"] / steps_per_launch
-        summary["salu_per_wave_per_step"] = pmc["SQ_INSTS_SALU"] / pmc["SQ_WAVES"] / steps_per_launch
+    if "SQ_INSTS_VALU" in pmc:
+        # per env group (the envs of one wavefront, 64 // segment pitch) and step: the
+        # persistent fused kernel runs fewer waves, each over several groups
+        sys.path.insert(0, os.path.join(ROOT, "mobile-env-gan_amd"))
+        from mobile_env.scenarios.registry import SCENARIOS
+        U = SCENARIOS[workload]["num_ues"]
+        pitch = 16 if 8 < U <= 16 and 64 // U == 4 else 32 if 16 < U <= 32 and 64 // U == 2 else U
+        groups = -(-envs // (64 // pitch))
+        summary["groups_per_launch"] = groups
+        summary["valu_per_group_step"] = pmc["SQ_INSTS_VALU"] / groups / steps_per_launch
+        summary["salu_per_group_step"] = pmc["SQ_INSTS_SALU"] / groups / steps_per_launch
+        summary["lds_per_group_step"] = pmc.get("SQ_INSTS_LDS", 0.0) / groups / steps_per_launch
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=2)
 

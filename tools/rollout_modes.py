@@ -12,7 +12,7 @@ import mobile_env  # noqa: E402
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 WL = sys.argv[2] if len(sys.argv) > 2 else "mobile-large-central-v0"
-W, K, S = 2000, 2000, 20
+W, K, S = 2000, int(os.environ.get("K", 2000)), 20
 
 
 def timed(fn):
@@ -28,8 +28,9 @@ def timed(fn):
     return a.elapsed_time(b) * 1e3 / K
 
 
-for mode in ("fused_overwrite", "rollout", "single", "rollout10", "rollout5", "rollout4",
-             "rollout2"):
+MODES = os.environ.get("MODES", "fused_overwrite,rollout,single,rollout10,rollout5,rollout4,"
+                                "rollout2").split(",")
+for mode in MODES:
     env = mobile_env.make(WL, num_envs=E, device="cuda:0", seed=1000,
                           fuse_steps=-1 if mode == "single" else 0)
     env.reset()
@@ -44,7 +45,8 @@ for mode in ("fused_overwrite", "rollout", "single", "rollout10", "rollout5", "r
     else:
         def fn():
             eng.step(S)
-    print(json.dumps({"mode": mode, "envs": E, "workload": WL, "us_per_step": timed(fn)}),
+    print(json.dumps({"lib": os.path.basename(os.environ.get("MEV_LIB", "libmev.so")),
+                      "mode": mode, "envs": E, "workload": WL, "us_per_step": timed(fn)}),
           flush=True)
     env.close()
     del traj
