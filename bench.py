@@ -20,9 +20,12 @@ Contract (see DESIGN.md "Measurement"):
   ranks time. Inputs are resident in HBM before timing starts.
 * roofline: algorithmic bytes per launch over the launch's average duration from HIP events
   on the stream the kernel runs on (around every launch; for one-step launches around every
-  chunk of 20, gaps included). One-step launch: E * (54*U + 61) (SURVEY.md 8d canonical:
-  state r+w 34 B/UE + outputs 20 B/UE; per env 61 B). Rollout launch of n steps: the outputs
-  of every step, E * n * (20*U + 5), plus the state read and written once, E * (34*U + 56).
+  chunk of 20, gaps included). Algorithmic bytes = SURVEY.md 8d's per-unit figure x the units
+  one launch processes: (54*U + 61) B per env-step (canonical: state r+w 34 B/UE + outputs
+  20 B/UE; per env 61 B) x E envs x the launch's steps (20 for a rollout launch). A rollout
+  keeps the env state in registers between its steps, so it moves fewer bytes than that:
+  `rollout_model_bytes_per_launch` = every step's outputs, E * n * (20*U + 5), plus the
+  canonical state read and written once, E * (34*U + 56); the PMC `traffic` is what it moved.
   traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
   (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
@@ -218,8 +221,7 @@ def main():
     if rank == 0:
         value = world * E * K / elapsed
         spl = CHUNK if fused else 1  # steps per launch
-        algo_bytes = E * (algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused else
-                          algorithmic_bytes_per_env_step(U, per_env_bs, B))
+        algo_bytes = E * spl * algorithmic_bytes_per_env_step(U, per_env_bs, B)
         launch_ms = kern_ms * spl
         achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
         traffic, rocprof_ms = load_profile(args.workload, E, args.launch)
@@ -245,6 +247,11 @@ def main():
                          "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                           if traffic else None),
                          "algorithmic_bytes_per_launch": algo_bytes,
+                         "algorithmic_bytes_per_env_step": algorithmic_bytes_per_env_step(
+                             U, per_env_bs, B),
+                         "rollout_model_bytes_per_launch": (
+                             E * algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused
+                             else None),
                          "steps_per_launch": spl,
                          "launch_ms": launch_ms,
                          "rocprof_launch_ms": rocprof_ms,

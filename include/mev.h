@@ -80,7 +80,7 @@ typedef struct mev_params {
   int32_t draw_table;        /* episode draw table (U <= 64, movement_reseed = 1): pairs per
                                 env precomputed from state0 by mev_reset / mev_prepare_draws
                                 (every episode of an env draws the same sequence); -1 auto
-                                (4U + 16), 0 off */
+                                (3U + 8), 0 off */
   int32_t fuse_steps;        /* mev_step(n > 1), U <= 64: 0 (auto) -> the n steps run in ONE
                                 launch with the env state in registers between them (outputs
                                 written every step, identical results); -1: n launches */

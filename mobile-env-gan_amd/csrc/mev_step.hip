@@ -288,8 +288,11 @@ __device__ __forceinline__ double utility_of(double rate, double cents, const KP
 
 constexpr int kPackedBlock = 256;
 constexpr int kWavesPerBlock = kPackedBlock / 64;
-// fused launches with the LDS association tables: 10-wave workgroups, two per CU (one LDS copy
-// of the <= ~65 KB tables per 10 waves; 5 waves per SIMD, the kernel's register limit)
+// fused launches with the LDS association tables: 8-wave workgroups, two per CU (one LDS copy
+// of the <= ~65 KB tables per 8 waves; LDS-limited to 4 waves per SIMD). Measured at 65,536
+// mobile-large envs (us per rollout step): 8 waves 15.7; 12 waves with <= 80 VGPRs (6 per
+// SIMD) 16.5 -- 6,144 resident waves do not divide the 32,768 env groups, and the extra
+// occupancy bought little; 10 waves 18.2 (two workgroups do not fit beside each other).
 #ifndef MEV_LDS_WAVES
 #define MEV_LDS_WAVES 8
 #endif
@@ -532,9 +535,9 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //   FUSED: one of several steps of a launch (mev_step(n), n > 1): the env state stays in
 //         registers between the steps (`cur` is updated; the caller stores it after the last
 //         step), the per-step outputs are written every step as in separate launches.
-//   FUSED steps defer their output stores (Pending): `pend` holds the previous step's
-//   outputs (for row prev_row of nrows; nothing valid before the first step) and receives
-//   this step's. `out` is then the base (row 0) of the buffers.
+//   FUSED steps write row `row` of `nrows` output rows (`out` is the base, row 0); without
+//   LDSA they defer their stores (Pending): `pend` holds the previous step's outputs (for row
+//   row - 1; nothing valid before the first step) and receives this step's.
 //   LDSA: (fused, shared layout) association from the LDS copy of the compact tables at
 //         `lblob` (KTables::lds_blob) instead of the L2 gather.
 template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, bool LDSA = false>
@@ -543,7 +546,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              const LaneMap& m, GroupIn& cur, int e,
                                              bool env_ok, int* __restrict__ hist,
                                              const int* __restrict__ ltab = nullptr,
-                                             Pending* pend = nullptr, int prev_row = 0,
+                                             Pending* pend = nullptr, int row = 0,
                                              int nrows = 1,
                                              const char* __restrict__ lblob = nullptr,
                                              u128* __restrict__ lpcg = nullptr) {
@@ -749,9 +752,11 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // `full` (no server) would otherwise carry the load as pending around the loop, and the
   // compiler's merged wait before its register is reused is vmcnt(0) -- which also waits for
   // every store just issued
-  if (FUSED) {
-    flush_pending<LEAN>(out, *pend, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)prev_row,
-                        (uint32_t)nrows);
+  // (LDSA: no gather, nothing to defer -- the step's own stores go out at its end)
+  constexpr bool DEFER = FUSED && !LDSA;
+  if (DEFER) {
+    flush_pending<LEAN>(out, *pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
+                        (uint32_t)max(row - 1, 0), (uint32_t)nrows);
     asm volatile("" ::"v"(srv), "v"(full));
   }
 
@@ -852,18 +857,24 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       out.qoe_stats[e] = a;
     }
   }
-  if (FUSED) {  // held back until the next step's gather (or the end of the launch)
-    pend->srv = srv;
-    pend->obs = obs;
-    pend->rate = rate;
-    pend->util = util_out;
-    pend->reward = reward_out;
-    pend->met = met;
-    pend->ui = (uint32_t)idx;
-    pend->e = e;
-    pend->valid = valid;
-    pend->lead = lead;
-    pend->done = t + 1 >= kp.t_end;
+  if (FUSED) {  // DEFER: held back until the next step's gather (or the end of the launch)
+    Pending cp;
+    cp.srv = srv;
+    cp.obs = obs;
+    cp.rate = rate;
+    cp.util = util_out;
+    cp.reward = reward_out;
+    cp.met = met;
+    cp.ui = (uint32_t)idx;
+    cp.e = e;
+    cp.valid = valid;
+    cp.lead = lead;
+    cp.done = t + 1 >= kp.t_end;
+    if (DEFER)
+      *pend = cp;
+    else
+      flush_pending<LEAN>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
+                          (uint32_t)nrows);
   }
   if (FUSED) {
     cur.t = t + 1;
@@ -982,10 +993,10 @@ __global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_
     const int nrows = traj ? nsteps : 1;
     for (int i = 0; i < nsteps; ++i)
       moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSA>(
-          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? max(i - 1, 0) : 0, nrows,
-          lblob, lpcg);
-    flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
-                        traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
+          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg);
+    if (!LDSA)  // the last step's deferred outputs
+      flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
+                          traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
     // the state after the last step
     if (env_ok && m.u < U)
       store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
@@ -1619,7 +1630,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
   c->kp.tab_m = 0;
   if (params->draw_table != 0 && params->movement_reseed && params->num_ues <= 64)
-    c->kp.tab_m = params->draw_table > 0 ? params->draw_table : 4 * params->num_ues + 16;
+    c->kp.tab_m = params->draw_table > 0 ? params->draw_table : 3 * params->num_ues + 8;
   if (c->kp.tab_m) {
     const size_t n = (size_t)params->num_envs * (size_t)c->kp.tab_m;
     if (c->kp.tab_m < params->num_ues || n >= ((size_t)1 << 28) ||

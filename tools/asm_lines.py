@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "mobile-env-gan_amd", "csrc", "mev_step.hip")
+SRC = os.environ.get('MEV_SRC', os.path.join(ROOT, 'mobile-env-gan_amd', 'csrc', 'mev_step.hip'))
 OUT = "/tmp/mev_step_lines.s"
 
 
