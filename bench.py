@@ -205,7 +205,10 @@ def main():
         chunk()
         b.record(stream)
     if world > 1:  # the one collective: final (reward, done) batch to every rank
-        gather_final(env.engine.reward, env.engine.done)
+        if traj is not None:  # the last step's row of the trajectory
+            gather_final(traj.reward[CHUNK - 1], traj.done[CHUNK - 1])
+        else:
+            gather_final(env.engine.reward, env.engine.done)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
