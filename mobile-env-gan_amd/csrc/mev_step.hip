@@ -298,9 +298,6 @@ constexpr int kWavesPerBlock = kPackedBlock / 64;
 #endif
 constexpr int kLdsWaves = MEV_LDS_WAVES;
 constexpr int kLdsBytesPerWG = 80 * 1024;
-#ifndef MEV_STORE_AUX
-#define MEV_STORE_AUX 0  // cache policy of the fused steps' output stores
-#endif
 
 
 // Sum of `v` over the lanes of one env segment that have `take` set (segment = lanes
@@ -390,6 +387,15 @@ __device__ __forceinline__ LaneMap lane_map(int lane, int P) {
   m.segmask = (P >= 64) ? ~0ull : (((1ull << P) - 1ull) << m.base);
   m.lt = (1ull << lane) - 1ull;
   return m;
+}
+
+// The env's bits of a wavefront ballot, at bit 0, for aligned segments (P = 16 or 32): one
+// 32-bit half of the ballot (a select between two scalar halves) or a 16-bit field of it --
+// cheaper than masking the 64-bit ballot with the lane's segment mask.
+template <int PC>
+__device__ __forceinline__ uint32_t seg_field(uint64_t b, const LaneMap& m) {
+  const uint32_t half = (m.base & 32) ? (uint32_t)(b >> 32) : (uint32_t)b;
+  return PC == 32 ? half : __builtin_amdgcn_ubfe(half, (uint32_t)(m.base & 16), 16u);
 }
 
 // Per-lane inputs of one env group. The loads are unconditional (env index clamped to a
@@ -509,14 +515,17 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
                  ndone = nrows * E;
   const v4u32 ob = {__float_as_uint(p.obs.x), __float_as_uint(p.obs.y),
                     __float_as_uint(p.obs.z), __float_as_uint(p.obs.w)};
+  // lane part of the offset (loop-invariant; one past the end for lanes without data: the
+  // buffer range check drops those, as voffset + soffset < 2^32 -- nrows * row bytes < 2^31)
+  // + the row as the scalar offset
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving, nsrv),
-                                        p.valid ? row * rsrv + 4u * p.ui : nsrv, 0, MEV_STORE_AUX);
+                                        p.valid ? 4u * p.ui : nsrv, row * rsrv, 0);
   __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
-                                         p.valid ? row * robs + 16u * p.ui : nobs, 0, MEV_STORE_AUX);
+                                         p.valid ? 16u * p.ui : nobs, row * robs, 0);
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
-                                        p.lead ? row * rrew + 4u * (uint32_t)p.e : nrew, 0, MEV_STORE_AUX);
+                                        p.lead ? 4u * (uint32_t)p.e : nrew, row * rrew, 0);
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
-                                       p.lead ? row * E + (uint32_t)p.e : ndone, 0, MEV_STORE_AUX);
+                                       p.lead ? (uint32_t)p.e : ndone, row * E, 0);
   if (!LEAN) {
     const KOut o = out_row(out, (int)E, (int)(EU / E), (int)row);
     if (p.valid) {
@@ -619,9 +628,15 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ------------
   const bool need = active && wp.x < 0;
   const uint64_t mneed_w = __ballot(need);
-  const uint64_t mneed = mneed_w & segmask;
-  const int tot = __popcll(mneed);  // draws of this env this step: 2 per waypoint
-  const int rank = __popcll(mneed & lt);
+  int tot, rank;  // draws of this env this step (2 per waypoint); this lane's rank among them
+  if constexpr (ROWS) {
+    const uint32_t f = seg_field<PC>(mneed_w, m);
+    tot = __popc(f);
+    rank = __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)u));
+  } else {
+    tot = __popcll(mneed_w & segmask);
+    rank = __popcll(mneed_w & segmask & lt);
+  }
   bool fell_back = false;  // wave-uniform: this step's draws came from the stream state
   if (mneed_w) {
     const int k = drawn + rank;  // this draw's pair index in the episode
@@ -795,8 +810,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
-  const uint64_t mact = __ballot(active) & segmask;
-  const int nact = __popcll(mact);
+  const int nact = ROWS ? __popc(seg_field<PC>(__ballot(active), m))
+                        : __popcll(__ballot(active) & segmask);
   const double sum_u = ROWS ? seg_sum_rows<PC>(util, active) : seg_sum(util, active, U, u);
   double sum_r = 0.0;
   if (want_metrics)
@@ -882,7 +897,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cur.drawn = drawn + tot;
     cur.s_ok = s_ok;
   }
-  return __ballot(own_fin) & segmask;  // the env's stream moved this step
+  // the env's stream moved this step
+  return ROWS ? seg_field<PC>(__ballot(own_fin), m) != 0u : (__ballot(own_fin) & segmask) != 0;
 }
 
 // Block -> env-range slot. Blocks are dealt round-robin over the 8 XCDs (observed placement,
@@ -1821,9 +1837,10 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
     const size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
-    // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^32 B)
+    // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^31 B,
+    // flush_pending)
     const int64_t row_bytes = 16 * (int64_t)kp.E * kp.U;
-    const int rows_max = traj ? (int)std::max<int64_t>(1, 0xFFFFFFFFll / row_bytes) : nsteps;
+    const int rows_max = traj ? (int)std::max<int64_t>(1, 0x7FFFFFFFll / row_bytes) : nsteps;
     for (int i0 = 0; i0 < nsteps; i0 += rows_max) {
       const int n = std::min(rows_max, nsteps - i0);
       kf<<<dim3(blocks), dim3(64 * nw), shmem_f, stream>>>(
