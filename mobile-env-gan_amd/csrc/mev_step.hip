@@ -67,13 +67,14 @@ struct KParams {
   float inv_w, inv_h; // obs normalisation
   int d2snap;         // largest integer d2 with sqrt(d2) <= velocity (arrival test)
   float move_band;    // tie band of the float32 movement fast path
+  float move_lim;     // 0.5 - move_band (exact)
   float u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale, u_offset;  // float32 utility
   int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
   float vel_f;
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
   int lds_assoc;      // bytes of the blob (multiple of 16)
-  int lds_st_off, lds_rank_off, lds_rate_off;  // byte offsets of its parts
+  int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off;  // byte offsets of its parts
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
 };
@@ -127,6 +128,7 @@ struct KTables {
   //   [lds_st_off, +64)        station coordinates x | y << 16 (16 slots)
   //   [lds_rank_off, ...)      uint2 {bits, prefix} per 32 squared distances: bit d of the
   //                            set S of sums of two squares <= d2max, prefix = |S below word|
+  //   [lds_r100_off, +576)     100 / n for n in [0, 64] (ResourceFair share, share_cents_r)
   //   [lds_rate_off, ...)      rate_full[d] for d in S, in increasing d (rank of d in S)
   // so full = rate[rank(d2)] with d2 to the serving station: the same float64 values as
   // `assoc`, from four LDS reads instead of one 16-byte gather from L2 per UE and step.
@@ -167,10 +169,6 @@ __device__ __forceinline__ uint64_t pcg_output(u128 s) {
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
 
-__device__ __forceinline__ u128 shfl_u128(u128 v, int src) {
-  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
-  return mk128(__shfl(lo, src), __shfl(hi, src));
-}
 
 // numpy Generator.uniform(0, span) is off + scale * next_double with next_double =
 // (next_uint64 >> 11) * 2^-53 (numpy/random/src/distributions/distributions.c); the reference
@@ -206,11 +204,6 @@ __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel)
                    (int)rint((double)pos.y + (vel * (double)dy) / nrm));
 }
 
-// true when q is farther than `band` from the nearest half-integer
-__device__ __forceinline__ bool clear_of_tie(float q, float band) {
-  const float f = q - floorf(q);  // exact
-  return fabsf(f - 0.5f) > band;
-}
 
 // Movement step. Arrival (|v| <= velocity) is the integer test d2 <= d2snap (sqrt is
 // correctly rounded and monotone). Otherwise the new coordinate is x + rint(q) with
@@ -238,9 +231,12 @@ __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) 
   const float r = __builtin_amdgcn_rsqf((float)d2);
   const float qx = kp.vel_f * (float)dx * r;
   const float qy = kp.vel_f * (float)dy * r;
-  if (clear_of_tie(qx, kp.move_band) && clear_of_tie(qy, kp.move_band)) {
-    pos.x += (int)rintf(qx);
-    pos.y += (int)rintf(qy);
+  // clear of a tie: |q - rint(q)| < 0.5 - move_band (<=> |frac(q) - 0.5| > move_band, with the
+  // rounding shared with the result; q - rint(q) is exact)
+  const float rx = rintf(qx), ry = rintf(qy);
+  if (fabsf(qx - rx) < kp.move_lim && fabsf(qy - ry) < kp.move_lim) {
+    pos.x += (int)rx;
+    pos.y += (int)ry;
   } else {
     pos = move_exact(pos, dx, dy, kp.vel);
   }
@@ -263,6 +259,14 @@ __device__ __forceinline__ double scaled_utility(double rate, const KParams& kp)
 // forms c = full * (100 / n) (within 2^-50 relative of the exact product) and rounds it
 // directly; only when c lies within 2^-46 relative of a half-integer are the two exact
 // float64 operations evaluated. Returns cents (an integer-valued double).
+// The same with r100 = 100 / n correctly rounded (from a table: no reciprocal on the device).
+__device__ __forceinline__ double share_cents_r(double full, double r100, int n) {
+  const double c = full * r100;
+  const double f = c - floor(c);
+  if (fabs(f - 0.5) > c * 0x1p-46) return rint(c);
+  return rint((full / (double)n) * 100.0);
+}
+
 __device__ __forceinline__ double share_cents(double full, int n) {
   // 100 / n to within 2 ulp: hardware reciprocal + two Newton steps (no table, no division)
   const double dn = (double)n;
@@ -347,12 +351,12 @@ __device__ __forceinline__ double seg_sum_rows(double v, bool take) {
 
 // Float32 form of the scaled BoundedLogUtility (used when no float64 utility output is
 // requested): clip(w1 log(w2 + r) / log(w3), lower, upper) with log via v_log_f32, then the
-// affine scale to [-1, 1]. Relative error ~1e-7 of the float64 value.
-__device__ __forceinline__ double utility_f32(double cents, const KParams& kp) {
+// affine scale to [-1, 1]; r = (float)cents * 0.01f is the obs rate. Relative error ~1e-7 of
+// the float64 value.
+__device__ __forceinline__ double utility_f32r(double cents, float r, const KParams& kp) {
   if (cents <= 0.0) return -1.0;  // rate <= 0 -> lower -> scaled -1
-  const float r = (float)cents * 0.01f;
   float ur = kp.u_log2_coef * __log2f(kp.u_w2f + r);
-  ur = fminf(fmaxf(ur, kp.u_lowerf), kp.u_upperf);
+  ur = __builtin_amdgcn_fmed3f(ur, kp.u_lowerf, kp.u_upperf);  // np.clip (ur is not NaN)
   return (double)(ur * kp.u_scale + kp.u_offset);
 }
 
@@ -801,12 +805,16 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
 
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
-  if (srv >= 0) cents = share_cents(full, n);
+  if (srv >= 0)
+    cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
+                                           lblob + kp.lds_r100_off + 8u * (uint32_t)n), n)
+                 : share_cents(full, n);
   if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
+  const float rate_f = (float)cents * 0.01f;  // the obs value
   double util = 0.0;
   if (active) {
     // exact float64 utility (table) when the caller asks for it, else the float32 form
-    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32(cents, kp);
+    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32r(cents, rate_f, kp);
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
@@ -827,8 +835,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 6. stores ----------------------------------------------------------------------
-  const float4 obs = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
-                                 (float)cents * 0.01f, (float)util);
+  const float4 obs = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, rate_f,
+                                 (float)util);
   const double util_out = active ? util : __builtin_nan("");
   if (valid && !FUSED) {
     const uint32_t ui = (uint32_t)idx;
@@ -897,8 +905,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cur.drawn = drawn + tot;
     cur.s_ok = s_ok;
   }
-  // the env's stream moved this step
-  return ROWS ? seg_field<PC>(__ballot(own_fin), m) != 0u : (__ballot(own_fin) & segmask) != 0;
+  return own_fin;  // this lane holds a new stream state of its env (the caller reduces)
 }
 
 // Block -> env-range slot. Blocks are dealt round-robin over the 8 XCDs (observed placement,
@@ -1017,6 +1024,9 @@ __global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_
     if (env_ok && m.u < U)
       store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
                make_int2(a.s.z, a.s.w));
+    // the env's stream moved during the launch: some lane of it owned a new state
+    const uint64_t mv = __ballot(moved);
+    moved = ROWS ? seg_field<PC>(mv, m) != 0u : (mv & m.segmask) != 0;
     if (env_ok && leader) {
       at(st.t, 4u * (uint32_t)e) = a.t;
       if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
@@ -1503,7 +1513,8 @@ static int build_lds_tables(mev_ctx* c) {
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t st_off = up16(((size_t)cells + 1) / 2);
   const size_t rank_off = st_off + 64;
-  const size_t rate_off = up16(rank_off + 8 * nwords);
+  const size_t r100_off = up16(rank_off + 8 * nwords);  // 100 / n for n in [0, 64]
+  const size_t rate_off = r100_off + 8 * 72;
   const size_t total = up16(rate_off + 8 * (size_t)count);
   if (total + kLdsWaves * lds_per_wave(kp) > (size_t)kLdsBytesPerWG) return MEV_OK;
   std::vector<double> full((size_t)d2max + 1);
@@ -1511,6 +1522,8 @@ static int build_lds_tables(mev_ctx* c) {
                     hipMemcpyDeviceToHost));
   std::vector<char> host(total - st_off, 0);  // stations, rank, rates (cell map: device)
   memcpy(host.data() + (rank_off - st_off), rank.data(), 8 * nwords);
+  double* r100 = reinterpret_cast<double*>(host.data() + (r100_off - st_off));
+  for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
   double* rates = reinterpret_cast<double*>(host.data() + (rate_off - st_off));
   for (int d = 0, k = 0; d <= d2max; ++d)
     if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) rates[k++] = full[(size_t)d];
@@ -1522,6 +1535,7 @@ static int build_lds_tables(mev_ctx* c) {
   kp.lds_st_off = (int)st_off;
   kp.lds_rank_off = (int)rank_off;
   kp.lds_rate_off = (int)rate_off;
+  kp.lds_r100_off = (int)r100_off;
   // persistent grid: every resident workgroup (the fewer of the two output variants)
   int cus = 0;
   MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -1593,6 +1607,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     kp.xcd_remap = xr ? atoi(xr) : 1;
   }
   kp.move_band = 0x1p-16f * (params->velocity > 1.0 ? (float)params->velocity : 1.0f);
+  kp.move_lim = 0.5f - kp.move_band;
   {  // arrival threshold and axis-parallel exactness (host IEEE float64 == device)
     const int d2_top = (params->width - 1) * (params->width - 1) +
                        (params->height - 1) * (params->height - 1);
