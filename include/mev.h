@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 7
+#define MEV_ABI_VERSION 8
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -137,6 +137,9 @@ void mev_destroy(mev_ctx* ctx);
 int mev_d2max(const mev_ctx* ctx);
 /* Number of env halves mev_step launches per step (1, or 2 on two streams; stream_split). */
 int mev_launch_parts(const mev_ctx* ctx);
+/* Bytes of the compact association tables rollout launches copy into LDS (shared layouts whose
+ * tables fit); 0: rollouts gather from the L2 association map. */
+int mev_lds_tables_bytes(const mev_ctx* ctx);
 /* Device pointer to the channel rate table (float64 [d2max+1]) -- for tests. */
 const double* mev_rate_table(const mev_ctx* ctx);
 /* Copy the first n entries of the channel rate table to dst (host or device memory,

@@ -524,8 +524,11 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
   // + the row as the scalar offset
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving, nsrv),
                                         p.valid ? 4u * p.ui : nsrv, row * rsrv, 0);
+  // (the 16-byte store takes its row in voffset: with an SGPR soffset the compiler omits the
+  // wait state between a > 8-byte store and a VALU write of its data registers, and on gfx950
+  // that write then corrupts the stored data -- seen as other values in a few obs rows)
   __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
-                                         p.valid ? 16u * p.ui : nobs, row * robs, 0);
+                                         (p.valid ? 16u * p.ui : nobs) + row * robs, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
                                         p.lead ? 4u * (uint32_t)p.e : nrew, row * rrew, 0);
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
@@ -1762,6 +1765,8 @@ void mev_destroy(mev_ctx* c) {
 int mev_d2max(const mev_ctx* c) { return c ? c->d2max : MEV_EINVAL; }
 
 int mev_launch_parts(const mev_ctx* c) { return c ? c->parts : MEV_EINVAL; }
+
+int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EINVAL; }
 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -22,7 +22,7 @@ MEV_EHIP = -1000
 MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
-EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts",
+EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_lds_tables_bytes",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations",
            "mev_reset", "mev_prepare_draws", "mev_step", "mev_rollout", "mev_strerror", "mev_last_hip_error")
@@ -90,6 +90,8 @@ def lib():
         L.mev_d2max.restype = C.c_int
         L.mev_launch_parts.argtypes = [C.c_void_p]
         L.mev_launch_parts.restype = C.c_int
+        L.mev_lds_tables_bytes.argtypes = [C.c_void_p]
+        L.mev_lds_tables_bytes.restype = C.c_int
         L.mev_rate_table.argtypes = [C.c_void_p]
         L.mev_rate_table.restype = C.c_void_p
         L.mev_copy_rate_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]

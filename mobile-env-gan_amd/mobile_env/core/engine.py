@@ -210,6 +210,11 @@ class StepEngine:
         """Env halves per step launch (1, or 2 on two streams)."""
         return int(self._lib.mev_launch_parts(self._ctx))
 
+    @property
+    def lds_tables_bytes(self) -> int:
+        """Bytes of the LDS association tables of rollout launches (0: L2 map gather)."""
+        return int(self._lib.mev_lds_tables_bytes(self._ctx))
+
     def rate_table(self):
         """Host copy (numpy float64) of the device-built channel table rate_full[0..d2max]."""
         import numpy as np
