@@ -228,13 +228,13 @@ __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) 
     else pos.y = (int)rint((double)pos.y + (dy > 0 ? q : -q));
     return;
   }
-  const float r = __builtin_amdgcn_rsqf((float)d2);
-  const float qx = kp.vel_f * (float)dx * r;
-  const float qy = kp.vel_f * (float)dy * r;
+  const float sc = kp.vel_f * __builtin_amdgcn_rsqf((float)d2);  // velocity / |v|
+  const float qx = (float)dx * sc;
+  const float qy = (float)dy * sc;
   // clear of a tie: |q - rint(q)| < 0.5 - move_band (<=> |frac(q) - 0.5| > move_band, with the
   // rounding shared with the result; q - rint(q) is exact)
   const float rx = rintf(qx), ry = rintf(qy);
-  if (fabsf(qx - rx) < kp.move_lim && fabsf(qy - ry) < kp.move_lim) {
+  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < kp.move_lim) {
     pos.x += (int)rx;
     pos.y += (int)ry;
   } else {
