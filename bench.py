@@ -20,12 +20,13 @@ Contract (see DESIGN.md "Measurement"):
   ranks time. Inputs are resident in HBM before timing starts.
 * roofline: algorithmic bytes per launch over the launch's average duration from HIP events
   on the stream the kernel runs on (around every launch; for one-step launches around every
-  chunk of 20, gaps included). Algorithmic bytes = SURVEY.md 8d's per-unit figure x the units
-  one launch processes: (54*U + 61) B per env-step (canonical: state r+w 34 B/UE + outputs
-  20 B/UE; per env 61 B) x E envs x the launch's steps (20 for a rollout launch). A rollout
-  keeps the env state in registers between its steps, so it moves fewer bytes than that:
-  `rollout_model_bytes_per_launch` = every step's outputs, E * n * (20*U + 5), plus the
-  canonical state read and written once, E * (34*U + 56); the PMC `traffic` is what it moved.
+  chunk of 20, gaps included). One-step launch: SURVEY.md 8d's per-unit figure, (54*U + 61) B
+  per env-step (canonical: state r+w 34 B/UE + outputs 20 B/UE; per env 61 B), x E. A rollout
+  launch of n steps keeps the env state in registers between its steps, so its algorithmic
+  bytes are every step's outputs, E * n * (20*U + 5), plus the canonical state read and
+  written once, E * (34*U + 56) -- counting the canonical per-step state round trip instead
+  (`canonical_equiv_*`) would put the rate above the HBM peak. The PMC `traffic` is what the
+  launch actually moved.
   traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
   (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
@@ -224,7 +225,9 @@ def main():
     if rank == 0:
         value = world * E * K / elapsed
         spl = CHUNK if fused else 1  # steps per launch
-        algo_bytes = E * spl * algorithmic_bytes_per_env_step(U, per_env_bs, B)
+        canon_bytes = E * spl * algorithmic_bytes_per_env_step(U, per_env_bs, B)
+        algo_bytes = (E * algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused
+                      else canon_bytes)
         launch_ms = kern_ms * spl
         achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
         traffic, rocprof_ms = load_profile(args.workload, E, args.launch)
@@ -250,11 +253,11 @@ def main():
                          "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                           if traffic else None),
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "algorithmic_bytes_per_env_step": algorithmic_bytes_per_env_step(
+                         "canonical_bytes_per_env_step": algorithmic_bytes_per_env_step(
                              U, per_env_bs, B),
-                         "rollout_model_bytes_per_launch": (
-                             E * algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused
-                             else None),
+                         "canonical_equiv_achieved": canon_bytes / (launch_ms * 1e-3) / 1e9,
+                         "canonical_equiv_frac": (canon_bytes / (launch_ms * 1e-3) / 1e9 /
+                                                  HBM_PEAK_GBS),
                          "steps_per_launch": spl,
                          "launch_ms": launch_ms,
                          "rocprof_launch_ms": rocprof_ms,
