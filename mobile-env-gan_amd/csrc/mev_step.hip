@@ -1056,11 +1056,13 @@ __global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_
       if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
       if (moved) {  // the state after the last pair drawn
         // (one global load from either the table entry or, without a table, the env's own
-        // state, selected by value: a select of addresses would put a.pa on the stack)
+        // state, selected by value: a select of addresses would put a.pa on the stack; the
+        // table index is clamped -- after fallback draws drawn > M, and the entry is unused)
         ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
         const ulonglong2 tv =
             kp.tab_m ? at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
-                          16u * ((uint32_t)e * (uint32_t)kp.tab_m + (uint32_t)max(a.drawn - 1, 0)))
+                          16u * ((uint32_t)e * (uint32_t)kp.tab_m +
+                                 (uint32_t)max(min(a.drawn, kp.tab_m) - 1, 0)))
                      : at(pcg2, 48u * (uint32_t)e);
         const u128 sl = lpcg[2 * m.seg];
         const ulonglong2 sf = a.s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
