@@ -74,7 +74,8 @@ struct KParams {
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
   int lds_assoc;      // bytes of the blob (multiple of 16)
-  int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off;  // byte offsets of its parts
+  int lds_mode;       // 1: station map + rank index; 2: + per-cell rank map (see packed_group)
+  int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off, lds_r16_off;  // byte offsets
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
 };
@@ -301,6 +302,13 @@ constexpr int kWavesPerBlock = kPackedBlock / 64;
 #define MEV_LDS_WAVES 8
 #endif
 constexpr int kLdsWaves = MEV_LDS_WAVES;
+// the two-read tables (LDSM 2: + a 2-byte rank per cell, ~141 KB for 200 x 200) take one
+// 16-wave workgroup per CU, the whole LDS
+constexpr int kLds2Waves = 16;
+constexpr int kLds2BytesPerWG = 160 * 1024;
+__host__ __device__ constexpr int lds_waves(int ldsm) {
+  return ldsm == 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
+}
 constexpr int kLdsBytesPerWG = 80 * 1024;
 
 
@@ -566,9 +574,11 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //   FUSED steps write row `row` of `nrows` output rows (`out` is the base, row 0); without
 //   LDSA they defer their stores (Pending): `pend` holds the previous step's outputs (for row
 //   row - 1; nothing valid before the first step) and receives this step's.
-//   LDSA: (fused, shared layout) association from the LDS copy of the compact tables at
-//         `lblob` (KTables::lds_blob) instead of the L2 gather.
-template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, bool LDSA = false>
+//   LDSM: (fused, shared layout) association from the LDS copy of the compact tables at
+//         `lblob` (KTables::lds_blob) instead of the L2 gather: 1 = station map + rank index
+//         (four dependent reads), 2 = station map + per-cell rank map (two parallel reads and
+//         the rate).
+template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
@@ -580,6 +590,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              u128* __restrict__ lpcg = nullptr) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
+  constexpr bool LDSA = LDSM != 0;
   const int U = UC ? UC : kp.U;
   const int P = PC ? PC : kp.U;
   const int u = m.u;
@@ -764,7 +775,13 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       const uint32_t nib =
           ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
           15u;
-      if (active && nib != 15u) {
+      if (LDSM == 2) {  // rank of the cell's d2 from the per-cell map, read beside the nibble
+        const uint32_t k = *reinterpret_cast<const uint16_t*>(lblob + kp.lds_r16_off + 2u * cell);
+        if (active && nib != 15u) {
+          srv = (int)nib;
+          full = *reinterpret_cast<const double*>(lblob + kp.lds_rate_off + 8u * k);
+        }
+      } else if (active && nib != 15u) {
         srv = (int)nib;
         const int sp = *reinterpret_cast<const int*>(lblob + kp.lds_st_off + 4u * nib);
         const int dx = pos.x - (int)(short)sp, dy = pos.y - (sp >> 16);
@@ -975,11 +992,12 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
 //   (shared layouts whose tables fit, KParams::lds_assoc), copied once; the grid is then sized
 //   to the resident workgroups (persistent: each wave takes groups g, g + T, g + 2T, ... of the
 //   T waves of the grid), so the copy is made once per workgroup slot, not once per group.
-template <bool PER_ENV_BS, bool LEAN, int UC, bool LDSA>
-__global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_packed(
+template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM>
+__global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj) {
   extern __shared__ int lds_all[];
-  constexpr int NW = LDSA ? kLdsWaves : kWavesPerBlock;  // waves per workgroup
+  constexpr bool LDSA = LDSM != 0;
+  constexpr int NW = lds_waves(LDSM);  // waves per workgroup
   int* lds_hist = lds_all;
   const char* lblob = nullptr;
   if (LDSA) {
@@ -1039,7 +1057,7 @@ __global__ __launch_bounds__(LDSA ? 64 * kLdsWaves : kPackedBlock) void k_steps_
     __builtin_amdgcn_s_waitcnt(0);
     const int nrows = traj ? nsteps : 1;
     for (int i = 0; i < nsteps; ++i)
-      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSA>(
+      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM>(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg);
     if (!LDSA)  // the last step's deferred outputs
       flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
@@ -1381,16 +1399,30 @@ __global__ void k_assoc_map(const int2* __restrict__ bs, int B, int W, int H, in
 // cell from the association map as 4 bits (15 = none), and the station coordinates. One thread
 // per byte of the cell map (two cells).
 __global__ void k_lds_map(const int2* __restrict__ bs, int B, int cells,
-                          const int4* __restrict__ map, uint8_t* __restrict__ blob, int st_off) {
+                          const int4* __restrict__ map, uint8_t* __restrict__ blob, int mode,
+                          int st_off, int r16_off, const uint2* __restrict__ rankw) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 16) {
+  if (mode == 1 && i < 16) {
     const int2 q = i < B ? bs[i] : make_int2(0, 0);
     reinterpret_cast<int*>(blob + st_off)[i] = (int)(((unsigned)q.x & 0xffffu) | ((unsigned)q.y << 16));
   }
   if (2 * i >= cells) return;
-  const int s0 = map[2 * i].x;
-  const int s1 = 2 * i + 1 < cells ? map[2 * i + 1].x : -1;
-  blob[i] = (uint8_t)((s0 < 0 ? 15 : s0) | ((s1 < 0 ? 15 : s1) << 4));
+  int sv[2];
+  for (int h = 0; h < 2; ++h) {
+    const int cl = 2 * i + h;
+    const int4 r = cl < cells ? map[cl] : make_int4(-1, 0, 0, 0);
+    sv[h] = r.x;
+    if (mode == 2 && cl < cells) {  // rank of the cell's d2 (to its station) in S
+      uint32_t k = 0;
+      if (r.x >= 0) {
+        const uint32_t d2 = (uint32_t)r.y;
+        const uint2 w = rankw[d2 >> 5];
+        k = w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
+      }
+      reinterpret_cast<uint16_t*>(blob + r16_off)[cl] = (uint16_t)k;
+    }
+  }
+  blob[i] = (uint8_t)((sv[0] < 0 ? 15 : sv[0]) | ((sv[1] < 0 ? 15 : sv[1]) << 4));
 }
 
 // Episode draw table of the envs with mask[e] (all if NULL): pair k of env e = draws 2k and
@@ -1449,6 +1481,7 @@ struct mev_ctx {
   double* util;
   int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
   int4* blob;     // its compact LDS form (KTables::lds_blob; null when it does not fit)
+  uint2* rankw;   // {bits, prefix} rank index of the sums of two squares <= d2max (global)
   int lds_wgs;    // resident workgroups of the LDSA fused kernel (CUs x per CU)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
   int fuse_steps;     // mev_step(n > 1): one fused launch (params.fuse_steps)
@@ -1503,7 +1536,7 @@ static int validate(const mev_params* p) {
 }
 
 typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
-static StepsKernel steps_kernel_for(bool per_env, bool lean, bool ldsa, int U);
+static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U);
 
 // LDS per workgroup of the fused LDSA kernel beyond the tables: each wave's n_b histogram and
 // episode draw table.
@@ -1520,8 +1553,10 @@ static size_t lds_per_wave(const KParams& kp) {
 static int build_lds_tables(mev_ctx* c) {
   KParams& kp = c->kp;
   kp.lds_assoc = 0;
-  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch
-  if ((sw && atoi(sw) == 0) || c->p.bs_per_env || kp.B > 15 || kp.U > 64) return MEV_OK;
+  kp.lds_mode = 0;
+  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 force a mode
+  const int want = sw ? atoi(sw) : 2;
+  if (want == 0 || c->p.bs_per_env || kp.B > 15 || kp.U > 64) return MEV_OK;
   const int cells = kp.W * kp.H;
   const int d2max = c->d2max;
   const size_t nwords = (size_t)d2max / 32 + 1;
@@ -1538,42 +1573,65 @@ static int build_lds_tables(mev_ctx* c) {
     rank[2 * w + 1] = count;
     count += (uint32_t)__builtin_popcount(bits[w]);
   }
+  // the rank index in global memory too: k_lds_map derives the per-cell ranks (mode 2)
+  if (hipMalloc(&c->rankw, 8 * nwords) != hipSuccess) return MEV_ENOMEM;
+  MEV_HIP(hipMemcpy(c->rankw, rank.data(), 8 * nwords, hipMemcpyHostToDevice));
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const size_t st_off = up16(((size_t)cells + 1) / 2);
-  const size_t rank_off = st_off + 64;
-  const size_t r100_off = up16(rank_off + 8 * nwords);  // 100 / n for n in [0, 64]
-  const size_t rate_off = r100_off + 8 * 72;
-  const size_t total = up16(rate_off + 8 * (size_t)count);
-  if (total + kLdsWaves * lds_per_wave(kp) > (size_t)kLdsBytesPerWG) return MEV_OK;
+  const size_t nib_bytes = up16(((size_t)cells + 1) / 2);
+  // mode 2: [cell nibbles][cell ranks u16][100/n][rates]; mode 1: [cell nibbles][stations]
+  // [rank index][100/n][rates]
+  size_t st_off = 0, rank_off = 0, r16_off = 0, r100_off, rate_off, total;
+  int mode = 0;
+  if (want >= 2 && count < 65536) {
+    r16_off = nib_bytes;
+    r100_off = up16(r16_off + 2 * (size_t)cells);
+    rate_off = r100_off + 8 * 72;
+    total = up16(rate_off + 8 * (size_t)count);
+    if (total + kLds2Waves * lds_per_wave(kp) <= (size_t)kLds2BytesPerWG) mode = 2;
+  }
+  if (!mode) {
+    st_off = nib_bytes;
+    rank_off = st_off + 64;
+    r100_off = up16(rank_off + 8 * nwords);  // 100 / n for n in [0, 64]
+    rate_off = r100_off + 8 * 72;
+    total = up16(rate_off + 8 * (size_t)count);
+    if (total + kLdsWaves * lds_per_wave(kp) > (size_t)kLdsBytesPerWG) return MEV_OK;
+    mode = 1;
+  }
   std::vector<double> full((size_t)d2max + 1);
   MEV_HIP(hipMemcpy(full.data(), c->rate_full, sizeof(double) * full.size(),
                     hipMemcpyDeviceToHost));
-  std::vector<char> host(total - st_off, 0);  // stations, rank, rates (cell map: device)
-  memcpy(host.data() + (rank_off - st_off), rank.data(), 8 * nwords);
-  double* r100 = reinterpret_cast<double*>(host.data() + (r100_off - st_off));
+  const size_t host_off = mode == 2 ? r100_off : st_off;  // the layout-independent part
+  std::vector<char> host(total - host_off, 0);
+  if (mode == 1) memcpy(host.data() + (rank_off - host_off), rank.data(), 8 * nwords);
+  double* r100 = reinterpret_cast<double*>(host.data() + (r100_off - host_off));
   for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
-  double* rates = reinterpret_cast<double*>(host.data() + (rate_off - st_off));
+  double* rates = reinterpret_cast<double*>(host.data() + (rate_off - host_off));
   for (int d = 0, k = 0; d <= d2max; ++d)
     if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) rates[k++] = full[(size_t)d];
   if (hipMalloc(&c->blob, total) != hipSuccess) return MEV_ENOMEM;
-  MEV_HIP(hipMemset(c->blob, 0xff, st_off));  // no station anywhere until a layout is set
-  MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + st_off, host.data(), host.size(),
+  MEV_HIP(hipMemset(c->blob, 0xff, nib_bytes));  // no station anywhere until a layout is set
+  if (mode == 2) MEV_HIP(hipMemset(reinterpret_cast<char*>(c->blob) + r16_off, 0, r100_off - r16_off));
+  MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + host_off, host.data(), host.size(),
                     hipMemcpyHostToDevice));
   kp.lds_assoc = (int)total;
+  kp.lds_mode = mode;
   kp.lds_st_off = (int)st_off;
   kp.lds_rank_off = (int)rank_off;
+  kp.lds_r16_off = (int)r16_off;
   kp.lds_rate_off = (int)rate_off;
   kp.lds_r100_off = (int)r100_off;
   // persistent grid: every resident workgroup (the fewer of the two output variants)
   int cus = 0;
   MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-  const size_t shmem = total + kLdsWaves * lds_per_wave(kp);
+  const int nw = lds_waves(mode);
+  const size_t shmem = total + nw * lds_per_wave(kp);
   int per = 1 << 30;
   for (int lean = 0; lean < 2; ++lean) {
     int n = 0;
     MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void*>(steps_kernel_for(false, lean != 0, true, kp.U)),
-        64 * kLdsWaves, shmem));
+        &n, reinterpret_cast<const void*>(steps_kernel_for(false, lean != 0, mode, kp.U)),
+        64 * nw, shmem));
     per = std::min(per, n);
   }
   c->lds_wgs = cus * per;
@@ -1581,6 +1639,7 @@ static int build_lds_tables(mev_ctx* c) {
     (void)hipFree(c->blob);
     c->blob = nullptr;
     kp.lds_assoc = 0;
+    kp.lds_mode = 0;
   }
   return MEV_OK;
 }
@@ -1778,6 +1837,7 @@ void mev_destroy(mev_ctx* c) {
   if (c->util) (void)hipFree(c->util);
   if (c->assoc) (void)hipFree(c->assoc);
   if (c->blob) (void)hipFree(c->blob);
+  if (c->rankw) (void)hipFree(c->rankw);
   if (c->tab_xy) (void)hipFree(c->tab_xy);
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
@@ -1842,21 +1902,21 @@ static StepKernel step_kernel_for(bool per_env, bool lean, int U) {
 }
 
 
-template <bool PER_ENV_BS, bool LEAN, bool LDSA>
+template <bool PER_ENV_BS, bool LEAN, int LDSM>
 static StepsKernel steps_kernel_u(int U) {
   switch (U) {
-    case 5: return k_steps_packed<PER_ENV_BS, LEAN, 5, LDSA>;
-    case 15: return k_steps_packed<PER_ENV_BS, LEAN, 15, LDSA>;
-    case 30: return k_steps_packed<PER_ENV_BS, LEAN, 30, LDSA>;
-    default: return k_steps_packed<PER_ENV_BS, LEAN, 0, LDSA>;
+    case 5: return k_steps_packed<PER_ENV_BS, LEAN, 5, LDSM>;
+    case 15: return k_steps_packed<PER_ENV_BS, LEAN, 15, LDSM>;
+    case 30: return k_steps_packed<PER_ENV_BS, LEAN, 30, LDSM>;
+    default: return k_steps_packed<PER_ENV_BS, LEAN, 0, LDSM>;
   }
 }
 
-static StepsKernel steps_kernel_for(bool per_env, bool lean, bool ldsa, int U) {
-  if (per_env)
-    return lean ? steps_kernel_u<true, true, false>(U) : steps_kernel_u<true, false, false>(U);
-  if (ldsa) return lean ? steps_kernel_u<false, true, true>(U) : steps_kernel_u<false, false, true>(U);
-  return lean ? steps_kernel_u<false, true, false>(U) : steps_kernel_u<false, false, false>(U);
+static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U) {
+  if (per_env) return lean ? steps_kernel_u<true, true, 0>(U) : steps_kernel_u<true, false, 0>(U);
+  if (ldsm == 2) return lean ? steps_kernel_u<false, true, 2>(U) : steps_kernel_u<false, false, 2>(U);
+  if (ldsm == 1) return lean ? steps_kernel_u<false, true, 1>(U) : steps_kernel_u<false, false, 1>(U);
+  return lean ? steps_kernel_u<false, true, 0>(U) : steps_kernel_u<false, false, 0>(U);
 }
 
 // Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
@@ -1877,8 +1937,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // stores); a launch that overwrites its outputs keeps the L2 gather (11.9 vs 15.1 us: the
     // stores stay in L2 and the tables' LDS cost occupancy, 4 vs 5 waves per SIMD)
     const bool ldsa = kp.lds_assoc > 0 && !c->p.bs_per_env && traj;
-    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsa, kp.U);
-    const int nw = ldsa ? kLdsWaves : kWavesPerBlock;
+    const int ldsm = ldsa ? kp.lds_mode : 0;
+    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
+    const int nw = lds_waves(ldsm);
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
     const size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
@@ -1963,7 +2024,8 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
     const int bytes = (cells + 1) / 2;
     hipLaunchKernelGGL(k_lds_map, dim3((bytes + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, cells, c->assoc,
-                       reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_st_off);
+                       reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_mode, c->kp.lds_st_off,
+                       c->kp.lds_r16_off, c->rankw);
     MEV_HIP(hipGetLastError());
   }
   return MEV_OK;
