@@ -12,14 +12,16 @@
 //      (metrics.py:25-28), the other metrics (metrics.py:5-21)
 //   -> time / done bookkeeping (base.py:280-291,407-409; arrival.py:28-36).
 //
-// Two launch shapes:
-//   * packed: U <= 64. A wavefront holds floor(64/U) envs, one lane per UE. Per-env
-//     reductions are ballot/popcount over the env's lane segment; no LDS atomics.
+// Launch shapes:
+//   * packed: U <= 64. A wavefront holds floor(64/U) envs, one lane per UE; per-env
+//     reductions are ballot/popcount/DPP over the env's lane segment. k_step_packed runs one
+//     step per launch (state loaded and stored every step); k_steps_packed runs n steps per
+//     launch with the state in registers (mev_step(n), mev_rollout), rollouts reading the
+//     association from LDS copies of compact tables in a persistent grid.
 //   * block:  64 < U <= 1024. One workgroup (ceil(U/64) waves) per env; per-BS counts
 //     with LDS atomics, RNG offsets by a workgroup scan.
-// Both are HBM-streaming kernels: per UE 8+8 B state read, 8+8 B state write,
-// 16 B obs + 4 B serving write; the channel table (<= 640 KB) stays in L2.
-//
+// One-step launches are HBM-streaming (per UE 8+8 B state, 16 B obs + 4 B serving); rollout
+// launches are bound by their instruction stream.
 // Numerics: the reference computes in float64 with numpy; every float64 op here keeps
 // the reference's operation order, the file is compiled with -ffp-contract=off, and
 // HIP's float64 '/', sqrt and rint are IEEE correctly rounded, so positions, serving
