@@ -183,3 +183,52 @@ def test_station_range_check():
     _check_station_range(lay, [1, 2])
     with pytest.raises(ValueError):
         _check_station_range(lay, [2, 2])
+
+
+def test_bench_byte_models():
+    """bench.py's byte models: SURVEY 8d's canonical 54 U + 61 B per env-step (1,681 B for
+    mobile-large), and the rollout launch's algorithmic bytes (every step's outputs + the state
+    read and written once) -- never above the canonical figure times the steps."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.algorithmic_bytes_per_env_step(30, False, 13) == 1681
+    assert bench.algorithmic_bytes_per_env_step(1024, True, 128) == 56381
+    for U in (5, 15, 30):
+        for n in (1, 2, 20):
+            r = bench.algorithmic_bytes_rollout(U, False, 3, n)
+            assert r == n * (20 * U + 5) + 34 * U + 56
+            assert r <= n * bench.algorithmic_bytes_per_env_step(U, False, 3)
+
+
+def test_sums_of_two_squares_rank_index():
+    """The LDS tables index the float64 rates by the rank of d2 in S = {a^2 + b^2 <= d2max}
+    (mev_step.hip build_lds_tables / k_lds_map): every squared integer distance is in S, and
+    the {bits, prefix} words give consecutive ranks (restated here on the host)."""
+    import numpy as np
+    d2max = 19362
+    s = set()
+    a = 0
+    while a * a <= d2max:
+        b = a
+        while a * a + b * b <= d2max:
+            s.add(a * a + b * b)
+            b += 1
+        a += 1
+    assert len(s) == 5101
+    nw = d2max // 32 + 1
+    bits = np.zeros(nw, np.uint64)
+    for d in s:
+        bits[d >> 5] |= np.uint64(1) << np.uint64(d & 31)
+    prefix = np.concatenate([[0], np.cumsum([bin(int(w)).count("1") for w in bits])[:-1]])
+    rank = lambda d: int(prefix[d >> 5]) + bin(int(bits[d >> 5]) & ((1 << (d & 31)) - 1)).count("1")
+    assert [rank(d) for d in sorted(s)] == list(range(len(s)))
+    rng = np.random.default_rng(0)
+    for _ in range(1000):  # positions and stations anywhere on a 200 x 200 map
+        dx, dy = rng.integers(-199, 200, 2)
+        d2 = int(dx * dx + dy * dy)
+        if d2 <= d2max:
+            assert d2 in s
