@@ -9,12 +9,15 @@ Contract (see DESIGN.md "Measurement"):
 * One step = one pass of the step over every env on the GPU (BASELINE.json configs[2]:
   65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank owns its own
   65,536 independent envs, seeds 1000 + global env index). By default steps are issued as
-  ``engine.rollout(20, traj)`` (mev_rollout, one episode): ONE launch of the fused multi-step
-  kernel, which keeps every env's state in registers between the 20 steps and writes EVERY
-  step's outputs (obs, serving, reward, done) to its own row of a [20, E, ...] trajectory
-  buffer in HBM -- the per-step outputs the reference's driver consumes every step
-  (base.py:261) -- bit-identical to 20 one-step launches. ``--launch single`` issues 20
-  one-step launches (mev_step(1), outputs overwritten) instead; ``split`` two env halves.
+  ``engine.rollout(40, traj)`` (mev_rollout, two 20-step episodes with the lazy auto-reset
+  between them, as the reference driver loop ``reset(); step() x 20`` repeated): ONE launch of
+  the fused multi-step kernel, which keeps every env's state in registers between the steps
+  and writes EVERY step's outputs (obs, serving, reward, done) to its own row of a
+  [40, E, ...] trajectory buffer in HBM -- the per-step outputs the reference's driver
+  consumes every step (base.py:261) -- bit-identical to 40 one-step launches (--chunk sets
+  the steps per launch; 20 = one episode: ~5 % slower, the launch's fill and drain and the
+  per-group prologue counted over fewer steps). ``--launch single`` issues one-step launches
+  (mev_step(1), outputs overwritten) instead; ``split`` two env halves.
 * Timed region: barrier + synchronize, K steps, the single final all-gather of the
   (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
   ranks time. Inputs are resident in HBM before timing starts.
@@ -99,7 +102,7 @@ def cpu_baseline(budget_s: float, procs: int):
                        f"(no JSON dump): {steps} env-steps in {wall:.1f} s")}
 
 
-def load_profile(workload: str, envs: int, launch: str = "fused"):
+def load_profile(workload: str, envs: int, launch: str = "fused", chunk: int = 40):
     """(HBM bytes per launch from the PMC passes, rocprofv3 average launch duration in ms of
     the timed region) of the committed profile of this workload and launch shape
     (tools/profile.sh + tools/pmc_summary.py), or Nones."""
@@ -109,7 +112,7 @@ def load_profile(workload: str, envs: int, launch: str = "fused"):
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
-    ent = d.get(f"{workload}@{envs}@{launch}") or {}
+    ent = d.get(f"{workload}@{envs}@{launch}" + (f"@{chunk}" if launch == "fused" else "")) or {}
     avg_ns = ent.get("rocprof_launch_avg_ns")
     return ent.get("hbm_bytes_per_launch"), (avg_ns * 1e-6 if avg_ns else None)
 
@@ -123,9 +126,12 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--launch", default="fused", choices=("fused", "single", "split"),
-                    help="fused: one rollout launch of 20 steps, every step's outputs kept "
-                         "(default); single: one launch per step; split: one launch per step "
+                    help="fused: one rollout launch per chunk of steps, every step's outputs "
+                         "kept (default); single: one launch per step; split: one launch per step "
                          "on two HIP streams (two env halves)")
+    ap.add_argument("--chunk", type=int, default=40,
+                    help="steps per engine call: per rollout launch (fused), or per C loop of "
+                         "one-step launches (single / split); 40 = two episodes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
@@ -171,7 +177,7 @@ def main():
     per_env_bs = env.engine.bs_per_env
     parts = env.engine.launch_parts
     env.reset()
-    CHUNK = 20  # steps per engine call (one episode)
+    CHUNK = args.chunk  # steps per engine call (two 20-step episodes by default)
     fused = args.launch == "fused" and env.engine.fused_steps
     traj = env.engine.trajectory(CHUNK) if args.launch == "fused" else None
 
@@ -230,7 +236,7 @@ def main():
                       else canon_bytes)
         launch_ms = kern_ms * spl
         achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
-        traffic, rocprof_ms = load_profile(args.workload, E, args.launch)
+        traffic, rocprof_ms = load_profile(args.workload, E, args.launch, CHUNK)
         out = {
             "metric": METRIC,
             "value": value,

@@ -24,7 +24,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CHUNK = 20  # bench.py: steps per engine.step call
+CHUNK = 40  # bench.py default --chunk: steps per engine call (rollout launch)
 
 FUSED_RE = re.compile(r"k_steps_packed<")
 SINGLE_RE = re.compile(r"k_step_packed<|k_step_block<(true|false), false>")
@@ -40,6 +40,7 @@ def main():
     out, tag = sys.argv[1], sys.argv[2]
     extra = sys.argv[3] if len(sys.argv) > 3 else ""
     workload, envs, steps, warmup, launch = "mobile-large-central-v0", 65536, 0, 0, "fused"
+    chunk = CHUNK
     toks = extra.split()
     for i, t in enumerate(toks[:-1]):
         if t == "--workload":
@@ -52,8 +53,10 @@ def main():
             warmup = int(toks[i + 1])
         elif t == "--launch":
             launch = toks[i + 1]
+        elif t == "--chunk":
+            chunk = int(toks[i + 1])
     kre = FUSED_RE if launch == "fused" else SINGLE_RE
-    steps = -(-steps // CHUNK) * CHUNK  # bench.py rounds up to whole chunks
+    steps = -(-steps // chunk) * chunk  # bench.py rounds up to whole chunks
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
 
@@ -72,7 +75,7 @@ def main():
     trace = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
                    for r in rows_of(os.path.join(out, "kt", "**", "*kernel_trace.csv"), "")
                    if kre.search(r.get("Kernel_Name", "")))
-    steps_per_launch = CHUNK if launch == "fused" else 1
+    steps_per_launch = chunk if launch == "fused" else 1
     parts = 2 if launch == "split" else 1
     n_timed = steps // steps_per_launch * parts
     if trace and n_timed:
@@ -84,7 +87,7 @@ def main():
         summary["step_interval_ns"] = span / steps
 
     # counters: per-dispatch averages over the kernel's dispatches of each pass (the fused
-    # warmup launches are whole 20-step chunks too, so every dispatch is the same work)
+    # warmup launches are whole chunks too, so every dispatch is the same work)
     pmc, ndisp = {}, {}
     for name in ("fetch", "write", "sq", "sq2"):
         vals = {}
@@ -121,7 +124,7 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     if "hbm_bytes_per_launch" in summary:
-        traffic[f"{workload}@{envs}@{launch}"] = {
+        traffic[f"{workload}@{envs}@{launch}" + (f"@{chunk}" if launch == "fused" else "")] = {
             "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
             "fetch_bytes_per_launch_corrected": summary["fetch_bytes_per_launch_corrected"],
             "write_bytes_per_launch": summary["write_bytes_per_launch"],

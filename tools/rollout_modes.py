@@ -12,7 +12,7 @@ import mobile_env  # noqa: E402
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 WL = sys.argv[2] if len(sys.argv) > 2 else "mobile-large-central-v0"
-W, K, S = 2000, int(os.environ.get("K", 2000)), 20
+W, K, S = 2000, int(os.environ.get("K", 2000)), int(os.environ.get("S", 20))
 
 
 def timed(fn):
