@@ -1030,20 +1030,26 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   for (int g = block_slot(kp.xcd_remap) * NW + wv; g < ngroups; g += gstride) {
     const int e = g * G + m.seg;
     const bool env_ok = (m.seg < G) && (e < kp.E);
-    if (kp.tab_m) {  // LDS-DMA copy, 256 B per instruction
+    // the group's inputs: the draw table (LDS-DMA, 256 B per instruction), the env state and
+    // the stream state, all issued before one wait
+    if (kp.tab_m) {
       const int n = G * kp.tab_m;
       const int* src = tb.tab_xy + (size_t)g * n;
       const int lim = min(n, (kp.E - g * G) * kp.tab_m);  // rows of envs that exist
       for (int c = 0; c * 64 < lim; ++c)
         if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
-      wait_vmem();
-      __builtin_amdgcn_wave_barrier();
     }
     GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
     const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
+    ulonglong2 pa = make_ulonglong2(0, 0), pb = pa;
     if (env_ok && leader) {
       ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-      const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
+      pa = at(pr, 48u * (uint32_t)e);
+      pb = at(pr, 48u * (uint32_t)e + 16u);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (env_ok && leader) {
       lpcg[2 * m.seg] = mk128(pa.x, pa.y);
       lpcg[2 * m.seg + 1] = mk128(pb.x, pb.y);
     }
