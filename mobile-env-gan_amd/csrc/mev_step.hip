@@ -769,11 +769,12 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     // shared layout: the association map holds, for every grid position of the map, the
     // serving station (or -1) and the full rate of that pair -- one 16-byte gather from an
     // L2-resident table replaces the per-station loop and the rate-table read
-    const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
     if (LDSA) {
       // the same association from LDS: station of the cell (4 bits), d2 to it, and the full
-      // rate at the rank of d2 in the set of sums of two squares (KTables::lds_blob)
-      const uint32_t cell = (uint32_t)(yi * kp.W + xi);
+      // rate at the rank of d2 in the set of sums of two squares (KTables::lds_blob). UE
+      // positions stay on the map (uniform draws in [0, W) x [0, H), moves toward waypoints
+      // there), so the cell index is only bounded, not clamped per coordinate
+      const uint32_t cell = min((uint32_t)(pos.y * kp.W + pos.x), (uint32_t)(kp.W * kp.H - 1));
       const uint32_t nib =
           ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
           15u;
@@ -793,6 +794,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         full = *reinterpret_cast<const double*>(lblob + kp.lds_rate_off + 8u * k);
       }
     } else {
+      const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
       const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));
       if (active) {
         srv = r.x;
