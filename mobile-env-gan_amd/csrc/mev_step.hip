@@ -565,6 +565,22 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
   }
 }
 
+// Registered scenarios with default parameters (medium, large; 200 x 200 map, default channel,
+// NoDeparture, draw table 3U + 8, the per-cell-rank LDS tables): their rollout launches run
+// an instance with these values as constants (SCN > 0; fewer kernel arguments held in
+// SGPRs: -3 % time per step), chosen on the host only when every value matches the context's.
+struct ScnConst {
+  int U, B, W, H, tab_m, hist_lds, t_end, arr_start, arr_exit, first_step_active;
+  int lds_r16_off, lds_r100_off, lds_rate_off, lds_assoc;
+};
+__host__ __device__ constexpr ScnConst scn_const(int scn) {
+  return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 20000, 100000, 100576, 141392}
+       : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 20000, 100000, 100576,
+                             141392}
+                  : ScnConst{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+}
+#define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
+
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
 //   UC:   U as a compile-time constant (0: runtime kp.U) -- folds the lane map, the segment
 //         reductions and the env indexing for the registered scenario sizes;
@@ -580,7 +596,7 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //         `lblob` (KTables::lds_blob) instead of the L2 gather: 1 = station map + rank index
 //         (four dependent reads), 2 = station map + per-cell rank map (two parallel reads and
 //         the rate).
-template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0>
+template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0, int SCN = 0>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
@@ -612,7 +628,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   u128* const slot = FUSED ? lpcg + 2 * m.seg : nullptr;
   u128 inc = FUSED ? (u128)0 : mk128(cur.pb.x, cur.pb.y);
   u128 s = FUSED ? (u128)0 : mk128(cur.pa.x, cur.pa.y);
-  const int M = kp.tab_m;  // wave-uniform
+  const int M = KPS(tab_m);  // wave-uniform
   int drawn = cur.drawn;
   bool s_ok = cur.s_ok;
 
@@ -624,7 +640,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   u128 s_fin = s;  // stream state after this lane's last draw
 
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
-  const bool reset_env = env_ok && t >= kp.t_end;  // every lane of the env, padding too
+  const bool reset_env = env_ok && t >= KPS(t_end);  // every lane of the env, padding too
   const bool do_reset = reset_env && valid;
   if (__ballot(reset_env)) {
     if (reset_env) t = 0;
@@ -654,8 +670,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
-  const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
-                      (kp.first_step_active || t != 0);
+  const bool active = valid && t >= KPS(arr_start) && t < KPS(arr_exit) &&
+                      (KPS(first_step_active) || t != 0);
 
   // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ------------
   const bool need = active && wp.x < 0;
@@ -745,10 +761,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     // index, as python's min() over the station dict)
     unsigned best = UINT_MAX;
     const s16x2 pu = {(short)pos.x, (short)pos.y};
-    const int nb = st.bs_count ? (valid ? st.bs_count[e] : 0) : kp.B;
-    const int2* bs = st.bs_xy + (size_t)e * kp.B;
+    const int nb = st.bs_count ? (valid ? st.bs_count[e] : 0) : KPS(B);
+    const int2* bs = st.bs_xy + (size_t)e * KPS(B);
     if (active && nb > 0) {
-      const int nb8 = (kp.B + 7) & ~7;  // wave-uniform trip count; j clamped to the last
+      const int nb8 = (KPS(B) + 7) & ~7;  // wave-uniform trip count; j clamped to the last
       for (int b0 = 0; b0 < nb8; b0 += 8) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -774,15 +790,15 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       // rate at the rank of d2 in the set of sums of two squares (KTables::lds_blob). UE
       // positions stay on the map (uniform draws in [0, W) x [0, H), moves toward waypoints
       // there), so the cell index is only bounded, not clamped per coordinate
-      const uint32_t cell = min((uint32_t)(pos.y * kp.W + pos.x), (uint32_t)(kp.W * kp.H - 1));
+      const uint32_t cell = min((uint32_t)(pos.y * KPS(W) + pos.x), (uint32_t)(KPS(W) * KPS(H) - 1));
       const uint32_t nib =
           ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
           15u;
       if (LDSM == 2) {  // rank of the cell's d2 from the per-cell map, read beside the nibble
-        const uint32_t k = *reinterpret_cast<const uint16_t*>(lblob + kp.lds_r16_off + 2u * cell);
+        const uint32_t k = *reinterpret_cast<const uint16_t*>(lblob + KPS(lds_r16_off) + 2u * cell);
         if (active && nib != 15u) {
           srv = (int)nib;
-          full = *reinterpret_cast<const double*>(lblob + kp.lds_rate_off + 8u * k);
+          full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
         }
       } else if (active && nib != 15u) {
         srv = (int)nib;
@@ -791,11 +807,11 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         const uint32_t d2 = (uint32_t)(dx * dx + dy * dy);
         const uint2 w = *reinterpret_cast<const uint2*>(lblob + kp.lds_rank_off + 8u * (d2 >> 5));
         const uint32_t k = w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
-        full = *reinterpret_cast<const double*>(lblob + kp.lds_rate_off + 8u * k);
+        full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
       }
     } else {
-      const int xi = min(max(pos.x, 0), kp.W - 1), yi = min(max(pos.y, 0), kp.H - 1);
-      const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * kp.W + xi));
+      const int xi = min(max(pos.x, 0), KPS(W) - 1), yi = min(max(pos.y, 0), KPS(H) - 1);
+      const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * KPS(W) + xi));
       if (active) {
         srv = r.x;
         full = __hiloint2double(r.w, r.z);
@@ -818,12 +834,12 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // ---- 3. n_b of the own serving BS ---------------------------------------------------
   const uint64_t mcon = __ballot(srv >= 0) & segmask;
   int n;
-  if (kp.hist_lds) {
+  if (KPS(hist_lds)) {
     // per-env histogram in the wavefront's own LDS slice [G][B]: zero, count, read back
     // (one wavefront's LDS instructions execute in order: no barrier)
-    int* h = hist + m.seg * kp.B;
+    int* h = hist + m.seg * KPS(B);
     if (env_ok)
-      for (int k = u; k < kp.B; k += P) h[k] = 0;
+      for (int k = u; k < KPS(B); k += P) h[k] = 0;
     __builtin_amdgcn_wave_barrier();
     if (srv >= 0) __hip_atomic_fetch_add(h + srv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __builtin_amdgcn_wave_barrier();
@@ -843,7 +859,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   double cents = 0.0, rate = 0.0;
   if (srv >= 0)
     cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
-                                           lblob + kp.lds_r100_off + 8u * (uint32_t)n), n)
+                                           lblob + KPS(lds_r100_off) + 8u * (uint32_t)n), n)
                  : share_cents(full, n);
   if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
   const float rate_f = (float)cents * 0.01f;  // the obs value
@@ -913,7 +929,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       at(st.t, 4u * (uint32_t)e) = t + 1;
       if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
       at(out.reward, 4u * (uint32_t)e) = reward_out;
-      at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= kp.t_end);
+      at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= KPS(t_end));
       if (want_metrics) out.metrics[e] = met;
     }
     if (want_qoe) {
@@ -937,7 +953,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cp.e = e;
     cp.valid = valid;
     cp.lead = lead;
-    cp.done = t + 1 >= kp.t_end;
+    cp.done = t + 1 >= KPS(t_end);
     if (DEFER)
       *pend = cp;
     else
@@ -971,7 +987,7 @@ __device__ __forceinline__ int block_slot(int remap) {
 template <bool PER_ENV_BS, bool LEAN, int UC>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb, int g0, int ngroups) {
-  extern __shared__ int lds_hist[];  // [waves][G][B] when kp.hist_lds
+  extern __shared__ int lds_hist[];  // [waves][G][B] when KPS(hist_lds)
   const int lane = threadIdx.x & 63;
   const int g = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= ngroups) return;
@@ -996,7 +1012,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
 //   (shared layouts whose tables fit, KParams::lds_assoc), copied once; the grid is then sized
 //   to the resident workgroups (persistent: each wave takes groups g, g + T, g + 2T, ... of the
 //   T waves of the grid), so the copy is made once per workgroup slot, not once per group.
-template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM>
+template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM, int SCN = 0>
 __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj) {
   extern __shared__ int lds_all[];
@@ -1006,14 +1022,14 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   const char* lblob = nullptr;
   if (LDSA) {
     // LDS-DMA copy (no registers): wave w moves 1 KB pieces w, w + NW, ...
-    const int n16 = kp.lds_assoc >> 4;
+    const int n16 = KPS(lds_assoc) >> 4;
     const int ln = threadIdx.x & 63;
     for (int c = (int)(threadIdx.x >> 6); c * 64 < n16; c += NW)
       if (c * 64 + ln < n16) glds(tb.lds_blob + c * 64 + ln, reinterpret_cast<int4*>(lds_all) + c * 64);
     wait_vmem();
     __syncthreads();
     lblob = reinterpret_cast<const char*>(lds_all);
-    lds_hist = lds_all + (kp.lds_assoc >> 2);
+    lds_hist = lds_all + (KPS(lds_assoc) >> 2);
   }
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -1026,18 +1042,18 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   // per wave: stream slots [G][2] u128 {state, inc}, the n_b histogram, the group's episode
   // draw tables (x, y pairs) in LDS for the whole launch (lds_per_wave)
   u128* lpcg = reinterpret_cast<u128*>(lds_hist) + wv * G * 2;
-  int* hist = lds_hist + NW * G * 8 + wv * G * kp.B * kp.hist_lds;
-  int* ltab = lds_hist + NW * G * 8 + NW * G * kp.B * kp.hist_lds + wv * G * kp.tab_m;
+  int* hist = lds_hist + NW * G * 8 + wv * G * KPS(B) * KPS(hist_lds);
+  int* ltab = lds_hist + NW * G * 8 + NW * G * KPS(B) * KPS(hist_lds) + wv * G * KPS(tab_m);
   const int gstride = LDSA ? (int)gridDim.x * NW : ngroups;
   for (int g = block_slot(kp.xcd_remap) * NW + wv; g < ngroups; g += gstride) {
     const int e = g * G + m.seg;
     const bool env_ok = (m.seg < G) && (e < kp.E);
     // the group's inputs: the draw table (LDS-DMA, 256 B per instruction), the env state and
     // the stream state, all issued before one wait
-    if (kp.tab_m) {
-      const int n = G * kp.tab_m;
+    if (KPS(tab_m)) {
+      const int n = G * KPS(tab_m);
       const int* src = tb.tab_xy + (size_t)g * n;
-      const int lim = min(n, (kp.E - g * G) * kp.tab_m);  // rows of envs that exist
+      const int lim = min(n, (kp.E - g * G) * KPS(tab_m));  // rows of envs that exist
       for (int c = 0; c * 64 < lim; ++c)
         if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
     }
@@ -1067,7 +1083,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     __builtin_amdgcn_s_waitcnt(0);
     const int nrows = traj ? nsteps : 1;
     for (int i = 0; i < nsteps; ++i)
-      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM>(
+      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN>(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg);
     if (!LDSA)  // the last step's deferred outputs
       flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
@@ -1081,16 +1097,16 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     moved = ROWS ? seg_field<PC>(mv, m) != 0u : (mv & m.segmask) != 0;
     if (env_ok && leader) {
       at(st.t, 4u * (uint32_t)e) = a.t;
-      if (kp.tab_m) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
+      if (KPS(tab_m)) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
       if (moved) {  // the state after the last pair drawn
         // (one global load from either the table entry or, without a table, the env's own
         // state, selected by value: a select of addresses would put a.pa on the stack; the
         // table index is clamped -- after fallback draws drawn > M, and the entry is unused)
         ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
         const ulonglong2 tv =
-            kp.tab_m ? at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
-                          16u * ((uint32_t)e * (uint32_t)kp.tab_m +
-                                 (uint32_t)max(min(a.drawn, kp.tab_m) - 1, 0)))
+            KPS(tab_m) ? at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
+                          16u * ((uint32_t)e * (uint32_t)KPS(tab_m) +
+                                 (uint32_t)max(min(a.drawn, KPS(tab_m)) - 1, 0)))
                      : at(pcg2, 48u * (uint32_t)e);
         const u128 sl = lpcg[2 * m.seg];
         const ulonglong2 sf = a.s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
@@ -1548,6 +1564,24 @@ static int validate(const mev_params* p) {
 typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
 static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U);
 
+// The registered scenario whose constants (scn_const) equal every corresponding value of the
+// context, or 0.
+static int match_scn(const KParams& kp) {
+  static const char* sw = getenv("MEV_SCN");  // dev A/B switch: 0 = always the generic kernel
+  if (sw && atoi(sw) == 0) return 0;
+  for (int s = 1; s <= 2; ++s) {
+    const ScnConst c = scn_const(s);
+    if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
+        kp.hist_lds == c.hist_lds && kp.t_end == c.t_end && kp.arr_start == c.arr_start &&
+        kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
+        kp.lds_mode == 2 && kp.lds_r16_off == c.lds_r16_off &&
+        kp.lds_r100_off == c.lds_r100_off && kp.lds_rate_off == c.lds_rate_off &&
+        kp.lds_assoc == c.lds_assoc)
+      return s;
+  }
+  return 0;
+}
+
 // LDS per workgroup of the fused LDSA kernel beyond the tables: each wave's n_b histogram and
 // episode draw table.
 static size_t lds_per_wave(const KParams& kp) {
@@ -1948,7 +1982,12 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // stores stay in L2 and the tables' LDS cost occupancy, 4 vs 5 waves per SIMD)
     const bool ldsa = kp.lds_assoc > 0 && !c->p.bs_per_env && traj;
     const int ldsm = ldsa ? kp.lds_mode : 0;
-    const StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
+    StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
+    if (ldsm == 2 && lean) {  // a registered scenario's constants (scn_const)
+      const int scn = match_scn(kp);
+      if (scn == 1) kf = k_steps_packed<false, true, 15, 2, 1>;
+      if (scn == 2) kf = k_steps_packed<false, true, 30, 2, 2>;
+    }
     const int nw = lds_waves(ldsm);
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
