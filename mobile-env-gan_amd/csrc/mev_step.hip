@@ -199,6 +199,30 @@ __device__ __forceinline__ u128 pcg_draw_pair_next(u128 s, u128 inc, double w, d
   return s2;
 }
 
+// Registered scenarios with default parameters (medium, large; 200 x 200 map, default channel,
+// NoDeparture, draw table 3U + 8, the per-cell-rank LDS tables): their rollout launches run
+// an instance with these values as constants (SCN > 0; fewer kernel arguments held in
+// SGPRs: -3 % time per step), chosen on the host only when every value matches the context's.
+struct ScnConst {
+  int U, B, W, H, tab_m, hist_lds, t_end, arr_start, arr_exit, first_step_active;
+  int lds_r16_off, lds_r100_off, lds_rate_off, lds_assoc;
+  // velocity 1.5, default utility: float32 values as bit patterns
+  int d2snap, axis_exact;
+  unsigned vel_f, move_lim, inv_w, inv_h, u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale,
+      u_offset;
+};
+__host__ __device__ constexpr ScnConst scn_const(int scn) {
+#define MEV_SCN_F32 2, 1, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
+                    0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u
+  return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 20000, 100000, 100576, 141392,
+                             MEV_SCN_F32}
+       : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 20000, 100000, 100576,
+                             141392, MEV_SCN_F32}
+                  : ScnConst{};
+}
+#define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
+#define KPSF(f) (SCN ? __builtin_bit_cast(float, scn_const(SCN).f) : kp.f)
+
 // Per-UE movement (movement.py:42-62), exact float64 form: the reference computes
 // position + velocity * v / |v| in float64, then np.round (half-to-even) and astype(int).
 __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel) {
@@ -216,28 +240,29 @@ __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel)
 // 2^-16 * max(1, velocity) (30x wider) of a half-integer -- where float32 could pick the
 // other integer, or half-to-even needs the exact value -- is the exact float64 form used. Axis-parallel
 // moves (q = +-velocity exactly) are done exactly in float64 (no division needed).
+template <int SCN = 0>
 __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
   const int dx = wp.x - pos.x;
   const int dy = wp.y - pos.y;
   const int d2 = dx * dx + dy * dy;
-  if (d2 <= kp.d2snap) {  // arrived: snap to waypoint and pop it
+  if (d2 <= KPS(d2snap)) {  // arrived: snap to waypoint and pop it
     pos = wp;
     wp = make_int2(-1, -1);
     return;
   }
-  if (kp.axis_exact && (dx == 0 || dy == 0)) {
+  if (KPS(axis_exact) && (dx == 0 || dy == 0)) {
     const double q = kp.vel;
     if (dy == 0) pos.x = (int)rint((double)pos.x + (dx > 0 ? q : -q));
     else pos.y = (int)rint((double)pos.y + (dy > 0 ? q : -q));
     return;
   }
-  const float sc = kp.vel_f * __builtin_amdgcn_rsqf((float)d2);  // velocity / |v|
+  const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);  // velocity / |v|
   const float qx = (float)dx * sc;
   const float qy = (float)dy * sc;
   // clear of a tie: |q - rint(q)| < 0.5 - move_band (<=> |frac(q) - 0.5| > move_band, with the
   // rounding shared with the result; q - rint(q) is exact)
   const float rx = rintf(qx), ry = rintf(qy);
-  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < kp.move_lim) {
+  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < KPSF(move_lim)) {
     pos.x += (int)rx;
     pos.y += (int)ry;
   } else {
@@ -375,11 +400,12 @@ __device__ __forceinline__ int seg_isum_rows(int x) {
 // requested): clip(w1 log(w2 + r) / log(w3), lower, upper) with log via v_log_f32, then the
 // affine scale to [-1, 1]; r = (float)cents * 0.01f is the obs rate. Relative error ~1e-7 of
 // the float64 value.
+template <int SCN = 0>
 __device__ __forceinline__ double utility_f32r(double cents, float r, const KParams& kp) {
   if (cents <= 0.0) return -1.0;  // rate <= 0 -> lower -> scaled -1
-  float ur = kp.u_log2_coef * __log2f(kp.u_w2f + r);
-  ur = __builtin_amdgcn_fmed3f(ur, kp.u_lowerf, kp.u_upperf);  // np.clip (ur is not NaN)
-  return (double)(ur * kp.u_scale + kp.u_offset);
+  float ur = KPSF(u_log2_coef) * __log2f(KPSF(u_w2f) + r);
+  ur = __builtin_amdgcn_fmed3f(ur, KPSF(u_lowerf), KPSF(u_upperf));  // np.clip (ur is not NaN)
+  return (double)(ur * KPSF(u_scale) + KPSF(u_offset));
 }
 
 // ------------------------------------------------------------------------------------
@@ -565,21 +591,6 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
   }
 }
 
-// Registered scenarios with default parameters (medium, large; 200 x 200 map, default channel,
-// NoDeparture, draw table 3U + 8, the per-cell-rank LDS tables): their rollout launches run
-// an instance with these values as constants (SCN > 0; fewer kernel arguments held in
-// SGPRs: -3 % time per step), chosen on the host only when every value matches the context's.
-struct ScnConst {
-  int U, B, W, H, tab_m, hist_lds, t_end, arr_start, arr_exit, first_step_active;
-  int lds_r16_off, lds_r100_off, lds_rate_off, lds_assoc;
-};
-__host__ __device__ constexpr ScnConst scn_const(int scn) {
-  return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 20000, 100000, 100576, 141392}
-       : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 20000, 100000, 100576,
-                             141392}
-                  : ScnConst{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-}
-#define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
 
 // One env group (floor(64/U) envs, one lane per UE) of the packed step kernel.
 //   UC:   U as a compile-time constant (0: runtime kp.U) -- folds the lane map, the segment
@@ -751,7 +762,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       else if (tot > 0 || reset_env) s_ok = false;
     }
   }
-  if (active) move_ue(pos, wp, kp);
+  if (active) move_ue<SCN>(pos, wp, kp);
 
   // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
   int srv = -1;
@@ -866,7 +877,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   double util = 0.0;
   if (active) {
     // exact float64 utility (table) when the caller asks for it, else the float32 form
-    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32r(cents, rate_f, kp);
+    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32r<SCN>(cents, rate_f, kp);
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
@@ -893,7 +904,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 6. stores ----------------------------------------------------------------------
-  const float4 obs = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, rate_f,
+  const float4 obs = make_float4((float)pos.x * KPSF(inv_w), (float)pos.y * KPSF(inv_h), rate_f,
                                  (float)util);
   const double util_out = active ? util : __builtin_nan("");
   if (valid && !FUSED) {
@@ -1566,6 +1577,11 @@ static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U);
 
 // The registered scenario whose constants (scn_const) equal every corresponding value of the
 // context, or 0.
+static unsigned fbits(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  return u;
+}
 static int match_scn(const KParams& kp) {
   static const char* sw = getenv("MEV_SCN");  // dev A/B switch: 0 = always the generic kernel
   if (sw && atoi(sw) == 0) return 0;
@@ -1576,7 +1592,12 @@ static int match_scn(const KParams& kp) {
         kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
         kp.lds_mode == 2 && kp.lds_r16_off == c.lds_r16_off &&
         kp.lds_r100_off == c.lds_r100_off && kp.lds_rate_off == c.lds_rate_off &&
-        kp.lds_assoc == c.lds_assoc)
+        kp.lds_assoc == c.lds_assoc && kp.d2snap == c.d2snap && kp.axis_exact == c.axis_exact &&
+        fbits(kp.vel_f) == c.vel_f && fbits(kp.move_lim) == c.move_lim &&
+        fbits(kp.inv_w) == c.inv_w && fbits(kp.inv_h) == c.inv_h &&
+        fbits(kp.u_log2_coef) == c.u_log2_coef && fbits(kp.u_w2f) == c.u_w2f &&
+        fbits(kp.u_lowerf) == c.u_lowerf && fbits(kp.u_upperf) == c.u_upperf &&
+        fbits(kp.u_scale) == c.u_scale && fbits(kp.u_offset) == c.u_offset)
       return s;
   }
   return 0;
