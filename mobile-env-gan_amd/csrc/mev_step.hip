@@ -244,7 +244,8 @@ template <int SCN = 0>
 __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
   const int dx = wp.x - pos.x;
   const int dy = wp.y - pos.y;
-  const int d2 = dx * dx + dy * dy;
+  // |dx|, |dy| <= map size < 2^23: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate)
+  const int d2 = __mul24(dx, dx) + __mul24(dy, dy);
   if (d2 <= KPS(d2snap)) {  // arrived: snap to waypoint and pop it
     pos = wp;
     wp = make_int2(-1, -1);
@@ -287,24 +288,36 @@ __device__ __forceinline__ double scaled_utility(double rate, const KParams& kp)
 // forms c = full * (100 / n) (within 2^-50 relative of the exact product) and rounds it
 // directly; only when c lies within 2^-46 relative of a half-integer are the two exact
 // float64 operations evaluated. Returns cents (an integer-valued double).
-// The same with r100 = 100 / n correctly rounded (from a table: no reciprocal on the device).
-__device__ __forceinline__ double share_cents_r(double full, double r100, int n) {
-  const double c = full * r100;
-  const double f = c - floor(c);
-  if (fabs(f - 0.5) > c * 0x1p-46) return rint(c);
-  return rint((full / (double)n) * 100.0);
+// Rounding of c = full * (100 / n) with the tie test in float32: d = c - rint(c) is exact in
+// float64 and its float32 conversion is within 2^-26, so 0.5 - |(float)d| > c 2^-46 + 2^-25
+// implies c is more than c 2^-46 away from a half-integer (the old bound) -- two float64
+// operations (rint, subtract) and two conversions instead of floor / fract / scale / compare in
+// float64. `cf` = (float)cents, the value the obs rate and the float32 utility use.
+__device__ __forceinline__ double cents_of(double c, double full, int n, float& cf) {
+  const double r = rint(c);
+  const float d = (float)(c - r);
+  const float rf = (float)r;
+  if (0.5f - fabsf(d) > __builtin_fmaf(rf, 0x1p-46f, 0x1p-25f)) {
+    cf = rf;
+    return r;
+  }
+  const double e = rint((full / (double)n) * 100.0);
+  cf = (float)e;
+  return e;
 }
 
-__device__ __forceinline__ double share_cents(double full, int n) {
+// The same with r100 = 100 / n correctly rounded (from a table: no reciprocal on the device).
+__device__ __forceinline__ double share_cents_r(double full, double r100, int n, float& cf) {
+  return cents_of(full * r100, full, n, cf);
+}
+
+__device__ __forceinline__ double share_cents(double full, int n, float& cf) {
   // 100 / n to within 2 ulp: hardware reciprocal + two Newton steps (no table, no division)
   const double dn = (double)n;
   double r = __builtin_amdgcn_rcp(dn);
   r = fma(r, fma(-dn, r, 1.0), r);
   r = fma(r, fma(-dn, r, 1.0), r);
-  const double c = full * (100.0 * r);
-  const double f = c - floor(c);
-  if (fabs(f - 0.5) > c * 0x1p-46) return rint(c);
-  return rint((full / dn) * 100.0);
+  return cents_of(full * (100.0 * r), full, n, cf);
 }
 
 // Scaled utility of a rounded rate. The utility depends on the rate only, and the rate is
@@ -401,11 +414,14 @@ __device__ __forceinline__ int seg_isum_rows(int x) {
 // affine scale to [-1, 1]; r = (float)cents * 0.01f is the obs rate. Relative error ~1e-7 of
 // the float64 value.
 template <int SCN = 0>
-__device__ __forceinline__ double utility_f32r(double cents, float r, const KParams& kp) {
-  if (cents <= 0.0) return -1.0;  // rate <= 0 -> lower -> scaled -1
-  float ur = KPSF(u_log2_coef) * __log2f(KPSF(u_w2f) + r);
+__device__ __forceinline__ double utility_f32r(float cents, float r, const KParams& kp) {
+  if (cents <= 0.f) return -1.0;  // rate <= 0 -> lower -> scaled -1
+  // a scenario's zero w2 / offset is not added (r > 0 and ur * scale != -0: the same bits)
+  constexpr bool no_w2 = SCN && scn_const(SCN).u_w2f == 0u;
+  constexpr bool no_off = SCN && scn_const(SCN).u_offset == 0u;
+  float ur = KPSF(u_log2_coef) * __log2f(no_w2 ? r : KPSF(u_w2f) + r);
   ur = __builtin_amdgcn_fmed3f(ur, KPSF(u_lowerf), KPSF(u_upperf));  // np.clip (ur is not NaN)
-  return (double)(ur * KPSF(u_scale) + KPSF(u_offset));
+  return (double)(no_off ? ur * KPSF(u_scale) : ur * KPSF(u_scale) + KPSF(u_offset));
 }
 
 // ------------------------------------------------------------------------------------
@@ -559,7 +575,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uin
 // lanes without data (padding lanes; non-leaders for the per-env rows) take the offset one
 // past the end, which the buffer range check drops. Without branches every path issues the
 // same VMEM ops, so the compiler's wait for the next gather can leave these stores in flight.
-template <bool LEAN>
+template <bool LEAN, bool SMALL = true>
 __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p, uint32_t E,
                                               uint32_t EU, uint32_t row, uint32_t nrows) {
   const uint32_t robs = 16u * EU, rsrv = 4u * EU, rrew = 4u * E;  // row bytes
@@ -577,10 +593,12 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
   // that write then corrupts the stored data -- seen as other values in a few obs rows)
   __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
                                          (p.valid ? 16u * p.ui : nobs) + row * robs, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
-                                        p.lead ? 4u * (uint32_t)p.e : nrew, row * rrew, 0);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
-                                       p.lead ? (uint32_t)p.e : ndone, row * E, 0);
+  if (SMALL) {  // (else staged in LDS by the caller: k_steps_packed, STG)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
+                                          p.lead ? 4u * (uint32_t)p.e : nrew, row * rrew, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
+                                         p.lead ? (uint32_t)p.e : ndone, row * E, 0);
+  }
   if (!LEAN) {
     const KOut o = out_row(out, (int)E, (int)(EU / E), (int)row);
     if (p.valid) {
@@ -607,7 +625,8 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //         `lblob` (KTables::lds_blob) instead of the L2 gather: 1 = station map + rank index
 //         (four dependent reads), 2 = station map + per-cell rank map (two parallel reads and
 //         the rate).
-template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0, int SCN = 0>
+template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0, int SCN = 0,
+          bool STG = false>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
@@ -616,7 +635,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              Pending* pend = nullptr, int row = 0,
                                              int nrows = 1,
                                              const char* __restrict__ lblob = nullptr,
-                                             u128* __restrict__ lpcg = nullptr) {
+                                             u128* __restrict__ lpcg = nullptr,
+                                             float* __restrict__ srew = nullptr,
+                                             uint8_t* __restrict__ sdone = nullptr) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   constexpr bool LDSA = LDSM != 0;
@@ -801,7 +822,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       // rate at the rank of d2 in the set of sums of two squares (KTables::lds_blob). UE
       // positions stay on the map (uniform draws in [0, W) x [0, H), moves toward waypoints
       // there), so the cell index is only bounded, not clamped per coordinate
-      const uint32_t cell = min((uint32_t)(pos.y * KPS(W) + pos.x), (uint32_t)(KPS(W) * KPS(H) - 1));
+      const uint32_t cell = min((uint32_t)(__mul24(pos.y, KPS(W)) + pos.x), (uint32_t)(KPS(W) * KPS(H) - 1));
       const uint32_t nib =
           ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
           15u;
@@ -815,7 +836,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         srv = (int)nib;
         const int sp = *reinterpret_cast<const int*>(lblob + kp.lds_st_off + 4u * nib);
         const int dx = pos.x - (int)(short)sp, dy = pos.y - (sp >> 16);
-        const uint32_t d2 = (uint32_t)(dx * dx + dy * dy);
+        const uint32_t d2 = (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
         const uint2 w = *reinterpret_cast<const uint2*>(lblob + kp.lds_rank_off + 8u * (d2 >> 5));
         const uint32_t k = w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
         full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
@@ -868,16 +889,17 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
 
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
+  float cents_f = 0.f;
   if (srv >= 0)
     cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
-                                           lblob + KPS(lds_r100_off) + 8u * (uint32_t)n), n)
-                 : share_cents(full, n);
+                                           lblob + KPS(lds_r100_off) + 8u * (uint32_t)n), n, cents_f)
+                 : share_cents(full, n, cents_f);
   if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
-  const float rate_f = (float)cents * 0.01f;  // the obs value
+  const float rate_f = cents_f * 0.01f;  // the obs value
   double util = 0.0;
   if (active) {
     // exact float64 utility (table) when the caller asks for it, else the float32 form
-    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32r<SCN>(cents, rate_f, kp);
+    util = exact_util ? utility_of(rate, cents, kp, tb.util) : utility_f32r<SCN>(cents_f, rate_f, kp);
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
@@ -965,11 +987,16 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     cp.valid = valid;
     cp.lead = lead;
     cp.done = t + 1 >= KPS(t_end);
-    if (DEFER)
+    if (DEFER) {
       *pend = cp;
-    else
-      flush_pending<LEAN>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
-                          (uint32_t)nrows);
+    } else {
+      flush_pending<LEAN, !STG>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
+                                (uint32_t)nrows);
+      if (STG && lead) {  // this step's row slot of the workgroup's staged per-env rows
+        srew[m.seg] = reward_out;
+        sdone[m.seg] = (uint8_t)cp.done;
+      }
+    }
   }
   if (FUSED) {
     cur.t = t + 1;
@@ -1023,9 +1050,29 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
 //   (shared layouts whose tables fit, KParams::lds_assoc), copied once; the grid is then sized
 //   to the resident workgroups (persistent: each wave takes groups g, g + T, g + 2T, ... of the
 //   T waves of the grid), so the copy is made once per workgroup slot, not once per group.
+// STG: the workgroup writes its staged per-env rows [row0, row0 + nr) x [e0, e0 + NWG) (reward
+// float32, done byte) with consecutive threads on consecutive envs, between two barriers (the
+// slots are complete before, and free for the next steps after).
+template <int NT, int NWG>
+__device__ __forceinline__ void flush_staged(const KOut& out, const float* srew,
+                                             const uint8_t* sdone, int E, int e0, int row0,
+                                             int nr) {
+  __syncthreads();
+  for (int q = threadIdx.x; q < nr * NWG; q += NT) {
+    const int r = q / NWG, j = q - r * NWG;
+    if (e0 + j < E) {
+      const uint32_t o = (uint32_t)(row0 + r) * (uint32_t)E + (uint32_t)(e0 + j);
+      at(out.reward, 4u * o) = srew[q];
+      at(out.done, o) = sdone[q];
+    }
+  }
+  __syncthreads();
+}
+
 template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM, int SCN = 0>
 __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
-    KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj) {
+    KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
+    int stage_rows) {
   extern __shared__ int lds_all[];
   constexpr bool LDSA = LDSM != 0;
   constexpr int NW = lds_waves(LDSM);  // waves per workgroup
@@ -1055,8 +1102,26 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   u128* lpcg = reinterpret_cast<u128*>(lds_hist) + wv * G * 2;
   int* hist = lds_hist + NW * G * 8 + wv * G * KPS(B) * KPS(hist_lds);
   int* ltab = lds_hist + NW * G * 8 + NW * G * KPS(B) * KPS(hist_lds) + wv * G * KPS(tab_m);
+  // STG (LDS-table trajectory launches, lean outputs): the per-env rows (reward float32, done
+  // byte) of the workgroup's NW * G consecutive envs are staged in LDS for stage_rows steps and
+  // then written by the whole workgroup as contiguous row pieces (128 B of reward per row for
+  // mobile-large) -- instead of every wavefront writing 2 x 4 B and 2 x 1 B pieces of each row
+  // (measured: those partial-line writes cost 1.5 of 13.5 us per step). The group loop is then
+  // uniform over the workgroup (its barriers): waves past the last group only take part in them.
+  constexpr bool STG = LDSM == 2 && LEAN && UC != 0;
+  constexpr int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
+  float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m)));
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(srew + (STG ? stage_rows * NWG : 0));
   const int gstride = LDSA ? (int)gridDim.x * NW : ngroups;
-  for (int g = block_slot(kp.xcd_remap) * NW + wv; g < ngroups; g += gstride) {
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  for (int gb = block_slot(kp.xcd_remap) * NW; gb < (STG ? ngroups : ngroups - wvu); gb += gstride) {
+    const int g = gb + wvu;
+    if (STG && g >= ngroups) {  // no group for this wave: its part of the flushes only
+      for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
+        flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i0 : 0,
+                                   min(stage_rows, nsteps - i0));
+      continue;
+    }
     const int e = g * G + m.seg;
     const bool env_ok = (m.seg < G) && (e < kp.E);
     // the group's inputs: the draw table (LDS-DMA, 256 B per instruction), the env state and
@@ -1093,9 +1158,14 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     // merged into the loop header, would also wait for the previous step's stores
     __builtin_amdgcn_s_waitcnt(0);
     const int nrows = traj ? nsteps : 1;
-    for (int i = 0; i < nsteps; ++i)
-      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN>(
-          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg);
+    for (int i = 0; i < nsteps; ++i) {
+      const int sr = STG ? i % stage_rows : 0;
+      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG>(
+          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg,
+          srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G);
+      if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
+        flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1);
+    }
     if (!LDSA)  // the last step's deferred outputs
       flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
                           traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
@@ -1294,7 +1364,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 
   // ---- 4. rate + utility -------------------------------------------------------------
   double cents = 0.0, rate = 0.0;
-  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv]);
+  float cents_f;
+  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv], cents_f);
   if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
   const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
   const bool want_metrics = out.metrics != nullptr;
@@ -1520,6 +1591,7 @@ struct mev_ctx {
   int4* blob;     // its compact LDS form (KTables::lds_blob; null when it does not fit)
   uint2* rankw;   // {bits, prefix} rank index of the sums of two squares <= d2max (global)
   int lds_wgs;    // resident workgroups of the LDSA fused kernel (CUs x per CU)
+  int stage_rows; // mode 2: rows of per-env outputs the lean fused kernel stages in LDS (STG)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
   int fuse_steps;     // mev_step(n > 1): one fused launch (params.fuse_steps)
   int* tab_xy;        // episode draw table (params.draw_table), see KTables
@@ -1572,7 +1644,7 @@ static int validate(const mev_params* p) {
   return MEV_OK;
 }
 
-typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int);
+typedef void (*StepsKernel)(KParams, KState, KOut, KTables, int, int, int, int);
 static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U);
 
 // The registered scenario whose constants (scn_const) equal every corresponding value of the
@@ -1607,6 +1679,13 @@ static int match_scn(const KParams& kp) {
 // episode draw table.
 static size_t lds_per_wave(const KParams& kp) {
   return sizeof(int) * (size_t)kp.envs_per_wave * (8 + (size_t)kp.B * kp.hist_lds + kp.tab_m);
+}
+// STG staging per wave and row (reward float32 + done byte per env), and for `rows` rows of
+// a workgroup of nw waves (only the compile-time-U kernels stage: U = 5, 15, 30)
+static size_t stage_bytes_per_row(const KParams& kp) { return 5 * (size_t)kp.envs_per_wave; }
+static bool stages(const KParams& kp) { return kp.U == 5 || kp.U == 15 || kp.U == 30; }
+static size_t stage_lds_bytes(const KParams& kp, int rows, int nw) {
+  return stages(kp) ? ((size_t)rows * nw * stage_bytes_per_row(kp) + 3) & ~(size_t)3 : 0;
 }
 
 // The layout-independent parts of the compact association tables (KTables::lds_blob): the
@@ -1652,7 +1731,10 @@ static int build_lds_tables(mev_ctx* c) {
     r100_off = up16(r16_off + 2 * (size_t)cells);
     rate_off = r100_off + 8 * 72;
     total = up16(rate_off + 8 * (size_t)count);
-    if (total + kLds2Waves * lds_per_wave(kp) <= (size_t)kLds2BytesPerWG) mode = 2;
+    // (+ at least one staged row of per-env outputs, k_steps_packed STG)
+    if (total + kLds2Waves * (lds_per_wave(kp) + stage_bytes_per_row(kp)) + 4 <=
+        (size_t)kLds2BytesPerWG)
+      mode = 2;
   }
   if (!mode) {
     st_off = nib_bytes;
@@ -1691,12 +1773,17 @@ static int build_lds_tables(mev_ctx* c) {
   MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const int nw = lds_waves(mode);
   const size_t shmem = total + nw * lds_per_wave(kp);
+  c->stage_rows = mode == 2 ? (int)(((size_t)kLds2BytesPerWG - shmem - 4) /
+                                    (nw * stage_bytes_per_row(kp)))
+                            : 0;
+  if (const char* sr = getenv("MEV_STAGE_ROWS"))  // test switch: shorter staging windows
+    if (atoi(sr) > 0) c->stage_rows = std::min(c->stage_rows, atoi(sr));
   int per = 1 << 30;
   for (int lean = 0; lean < 2; ++lean) {
     int n = 0;
     MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &n, reinterpret_cast<const void*>(steps_kernel_for(false, lean != 0, mode, kp.U)),
-        64 * nw, shmem));
+        64 * nw, shmem + (lean ? stage_lds_bytes(kp, c->stage_rows, nw) : 0)));
     per = std::min(per, n);
   }
   c->lds_wgs = cus * per;
@@ -2012,15 +2099,18 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const int nw = lds_waves(ldsm);
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
-    const size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
+    size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
+    const bool stg = ldsm == 2 && lean && stages(kp);  // k_steps_packed STG
     // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^31 B,
     // flush_pending)
     const int64_t row_bytes = 16 * (int64_t)kp.E * kp.U;
     const int rows_max = traj ? (int)std::max<int64_t>(1, 0x7FFFFFFFll / row_bytes) : nsteps;
     for (int i0 = 0; i0 < nsteps; i0 += rows_max) {
       const int n = std::min(rows_max, nsteps - i0);
-      kf<<<dim3(blocks), dim3(64 * nw), shmem_f, stream>>>(
-          kp, ks, traj ? out_row(ko, kp.E, kp.U, i0) : ko, tb, groups, n, traj ? 1 : 0);
+      const int srows = stg ? std::min(c->stage_rows, n) : 1;
+      kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
+           stream>>>(kp, ks, traj ? out_row(ko, kp.E, kp.U, i0) : ko, tb, groups, n,
+                     traj ? 1 : 0, srows);
     }
     MEV_HIP(hipGetLastError());
     return MEV_OK;

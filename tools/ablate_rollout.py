@@ -21,6 +21,15 @@ EDITS = {
                  "  } else if (false) {\n    // lanes of the segment with the same index")],
     "no_rate": [("    cents = LDSA ? share_cents_r(full,", "    cents = LDSA ? (double)(long)(full * n) + 0 * share_cents_r(full,")],
     "no_util": [("utility_f32r(cents, rate_f, kp);", "(double)(rate_f * 0.001f);")],
+    # the trajectory stores still issued, with every lane's offset out of range (dropped by
+    # the buffer range check): compute with no write traffic
+    "oob_small": [("p.lead ? 4u * (uint32_t)p.e : nrew", "nrew + 0 * p.e"),
+                  ("p.lead ? (uint32_t)p.e : ndone", "ndone + 0 * p.e")],
+    "oob_obs": [("(p.valid ? 16u * p.ui : nobs) + row * robs", "nobs + 0 * p.ui + row * robs")],
+    "oob_all": [("p.lead ? 4u * (uint32_t)p.e : nrew", "nrew + 0 * p.e"),
+                ("p.lead ? (uint32_t)p.e : ndone", "ndone + 0 * p.e"),
+                ("(p.valid ? 16u * p.ui : nobs) + row * robs", "nobs + 0 * p.ui + row * robs"),
+                ("p.valid ? 4u * p.ui : nsrv, row * rsrv", "nsrv + 0 * p.ui, row * rsrv")],
     "no_reward": [("  const int isum_u = ISUM ? seg_isum_rows<PC>(active ? (int)((float)util * 0x1p25f) : 0) : 0;",
                    "  const int isum_u = ISUM ? (int)((float)util * 0x1p25f) : 0;")],
 }
@@ -35,7 +44,8 @@ def build(name, edits):
     tmp = f"/tmp/ablate_{name}.hip"
     open(tmp, "w").write(s)
     return subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                             "-ffp-contract=off", "-fPIC", "-shared", f"-I{ROOT}/include", "-o",
+                             "-ffp-contract=off", "-fPIC", "-shared", "-mllvm",
+                             "-amdgpu-sched-strategy=max-ilp", f"-I{ROOT}/include", "-o",
                              os.path.join(OUT, f"libmev_ab_{name}.so"), tmp],
                             stderr=subprocess.DEVNULL)
 
