@@ -554,6 +554,10 @@ typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 // s_waitcnt vmcnt(0) only (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait on those)
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// Lane mask of a bool: the ballot builtin on the i1 itself (HIP's __ballot takes an int, and
+// the compiler then materialises compound conditions as v_cndmask + v_cmp before the ballot)
+__device__ __forceinline__ uint64_t bal(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
 // LDS-DMA: this lane's element `src` to lds_base + lane * sizeof(T) (lds_base wave-uniform);
 // complete after vmcnt(0)
 typedef const __attribute__((address_space(1))) void* gptr_t;
@@ -637,7 +641,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              const char* __restrict__ lblob = nullptr,
                                              u128* __restrict__ lpcg = nullptr,
                                              float* __restrict__ srew = nullptr,
-                                             uint8_t* __restrict__ sdone = nullptr) {
+                                             uint8_t* __restrict__ sdone = nullptr,
+                                             uint64_t envok_wf = 0, uint64_t valid_wf = 0) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   constexpr bool LDSA = LDSM != 0;
@@ -672,9 +677,14 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   u128 s_fin = s;  // stream state after this lane's last draw
 
   // ---- lazy auto-reset at the start of the step after the episode ended ---------------
+  // (wave masks: the ballot of one compare, ANDed in SALU with a loop-invariant mask -- the
+  // ballot of a compound condition costs a v_cndmask + v_cmp)
+  // (fused: the caller's, from before its step loop -- ballots are not hoisted out of it)
+  const uint64_t envok_w = FUSED ? envok_wf : bal(env_ok);
+  const uint64_t valid_w = FUSED ? valid_wf : bal(valid);
   const bool reset_env = env_ok && t >= KPS(t_end);  // every lane of the env, padding too
   const bool do_reset = reset_env && valid;
-  if (__ballot(reset_env)) {
+  if (bal(t >= KPS(t_end)) & envok_w) {
     if (reset_env) t = 0;
     if (M) {  // initial positions = the episode's first U pairs (draw table)
       if (reset_env) drawn = U;
@@ -706,8 +716,11 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                       (KPS(first_step_active) || t != 0);
 
   // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ------------
+  const uint64_t act_w =
+      bal(t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0)) &
+      valid_w;
   const bool need = active && wp.x < 0;
-  const uint64_t mneed_w = __ballot(need);
+  const uint64_t mneed_w = bal(wp.x < 0) & act_w;
   int tot, rank;  // draws of this env this step (2 per waypoint); this lane's rank among them
   if constexpr (ROWS) {
     const uint32_t f = seg_field<PC>(mneed_w, m);
@@ -720,7 +733,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   bool fell_back = false;  // wave-uniform: this step's draws came from the stream state
   if (mneed_w) {
     const int k = drawn + rank;  // this draw's pair index in the episode
-    if (M && __ballot(need && k >= M) == 0) {
+    if (M && (bal(k >= M) & mneed_w) == 0) {
       // draw table: every drawing lane of the wavefront finds its pair precomputed (fused
       // launches read the wavefront's copy in LDS and track only `drawn`)
       if (need) {
@@ -761,7 +774,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       }
       // common case: every drawing lane of the wave is the first of its env and no reset
       // came before -> two steps of the constant multiplier instead of a table jump
-      if (__ballot(need && (rank | koff)) == 0) {
+      if ((bal((rank | koff) != 0) & mneed_w) == 0) {
         if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, wp.x, wp.y);
       } else {
         if (need)
@@ -864,7 +877,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 3. n_b of the own serving BS ---------------------------------------------------
-  const uint64_t mcon = __ballot(srv >= 0) & segmask;
+  const uint64_t mcon = bal(srv >= 0) & segmask;
   int n;
   if (KPS(hist_lds)) {
     // per-env histogram in the wavefront's own LDS slice [G][B]: zero, count, read back
@@ -881,7 +894,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     uint64_t match = mcon;
     for (int bit = 0; bit < kp.srv_bits; ++bit) {
       const bool on = (srv >> bit) & 1;
-      const uint64_t mb = __ballot(on);
+      const uint64_t mb = bal(on);
       match &= on ? mb : ~mb;
     }
     n = (int)__popcll(match);
@@ -903,8 +916,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
-  const int nact = ROWS ? __popc(seg_field<PC>(__ballot(active), m))
-                        : __popcll(__ballot(active) & segmask);
+  const int nact = ROWS ? __popc(seg_field<PC>(act_w, m)) : __popcll(act_w & segmask);
   // lean path, aligned segments: the utilities (float32 values in [-1, 1]) summed as 2^-25
   // fixed point in int32 -- one DPP add per level instead of two moves and a float64 add;
   // error <= 2^-25 per UE, 1e-8 on the mean, below the float32 reward's own rounding
@@ -922,7 +934,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     const double q = rint(util * 100.0) / 100.0;
     sum_q = ROWS ? seg_sum_rows<PC>(q, active) : seg_sum(q, active, U, u);
     sum_q2 = ROWS ? seg_sum_rows<PC>(q * q, active) : seg_sum(q * q, active, U, u);
-    nlow = (int)__popcll(__ballot(active && q < kp.qoe_low) & segmask);
+    nlow = (int)__popcll(bal(active && q < kp.qoe_low) & segmask);
   }
 
   // ---- 6. stores ----------------------------------------------------------------------
@@ -939,6 +951,20 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
     if (!LEAN && out.util64) out.util64[idx] = util_out;
+  }
+  if (FUSED && STG) {  // the per-UE rows now, before the leaders' reward branch (issued after
+    // it, the compiler duplicates the stores into both sides: twice the store instructions,
+    // each half a row)
+    Pending up;
+    up.srv = srv;
+    up.obs = obs;
+    up.ui = (uint32_t)idx;
+    up.valid = valid;
+    up.lead = up.done = false;
+    up.e = 0;
+    up.reward = 0.f;
+    flush_pending<LEAN, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
+                               (uint32_t)nrows);
   }
   const bool lead = env_ok && leader;
   float reward_out = 0.f;
@@ -990,8 +1016,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     if (DEFER) {
       *pend = cp;
     } else {
-      flush_pending<LEAN, !STG>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
-                                (uint32_t)nrows);
+      if (!STG)
+        flush_pending<LEAN>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
+                            (uint32_t)nrows);
       if (STG && lead) {  // this step's row slot of the workgroup's staged per-env rows
         srew[m.seg] = reward_out;
         sdone[m.seg] = (uint8_t)cp.done;
@@ -1158,11 +1185,12 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     // merged into the loop header, would also wait for the previous step's stores
     __builtin_amdgcn_s_waitcnt(0);
     const int nrows = traj ? nsteps : 1;
+    const uint64_t envok_w = bal(env_ok), valid_w = bal(env_ok && m.u < U);
     for (int i = 0; i < nsteps; ++i) {
       const int sr = STG ? i % stage_rows : 0;
       moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG>(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg,
-          srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G);
+          srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w);
       if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
         flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1);
     }
@@ -1174,7 +1202,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
       store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
                make_int2(a.s.z, a.s.w));
     // the env's stream moved during the launch: some lane of it owned a new state
-    const uint64_t mv = __ballot(moved);
+    const uint64_t mv = bal(moved);
     moved = ROWS ? seg_field<PC>(mv, m) != 0u : (mv & m.segmask) != 0;
     if (env_ok && leader) {
       at(st.t, 4u * (uint32_t)e) = a.t;
@@ -1295,8 +1323,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 
   // ---- 1. movement: workgroup exclusive scan of "needs waypoint" in ue_id order -------
   const bool need = active && wp.x < 0;
-  const uint64_t mneed = __ballot(need);
-  const uint64_t mact = __ballot(active);
+  const uint64_t mneed = bal(need);
+  const uint64_t mact = bal(active);
   if (lane == 0) {
     lds_wtot[0][w] = __popcll(mneed);
     lds_wtot[1][w] = __popcll(mact);
@@ -1356,7 +1384,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 
   // ---- 3. per-BS counts via LDS atomics ---------------------------------------------
   if (srv >= 0) atomicAdd(&lds_cnt[srv], 1);
-  const uint64_t mcon = __ballot(srv >= 0);
+  const uint64_t mcon = bal(srv >= 0);
   if (lane == 0) lds_wtot[2][w] = __popcll(mcon);
   __syncthreads();
   const int tot_con =
@@ -1391,7 +1419,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       lds_sum[3][w] = sq2;
     }
   }
-  const uint64_t mlow = __ballot(want_qoe && active && q < kp.qoe_low);
+  const uint64_t mlow = bal(want_qoe && active && q < kp.qoe_low);
   if (lane == 0) lds_wtot[0][w] = __popcll(mlow);  // the need counts were read above
   __syncthreads();
 

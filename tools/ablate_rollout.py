@@ -16,11 +16,11 @@ EDITS = {
     "no_assoc": [("      if (active && nib != 15u) {",
                   "      if (active && nib != 15u) { srv = (int)nib; full = 1e7 + cell; }\n"
                   "      if (false) {")],
-    "no_hist": [("  if (kp.hist_lds) {", "  n = srv >= 0 ? 1 + (srv & 3) : 0;\n  if (false) {"),
+    "no_hist": [("  if (KPS(hist_lds)) {", "  n = srv >= 0 ? 1 + (srv & 3) : 0;\n  if (false) {"),
                 ("  } else {\n    // lanes of the segment with the same index",
                  "  } else if (false) {\n    // lanes of the segment with the same index")],
-    "no_rate": [("    cents = LDSA ? share_cents_r(full,", "    cents = LDSA ? (double)(long)(full * n) + 0 * share_cents_r(full,")],
-    "no_util": [("utility_f32r(cents, rate_f, kp);", "(double)(rate_f * 0.001f);")],
+    "no_rate": [("    cents = LDSA ? share_cents_r(full,", "    cents_f = (float)full * n; cents = LDSA ? (double)(long)(full * n) + 0 * share_cents_r(full,")],
+    "no_util": [("utility_f32r<SCN>(cents_f, rate_f, kp);", "(double)(rate_f * 0.001f);")],
     # the trajectory stores still issued, with every lane's offset out of range (dropped by
     # the buffer range check): compute with no write traffic
     "oob_small": [("p.lead ? 4u * (uint32_t)p.e : nrew", "nrew + 0 * p.e"),
