@@ -987,8 +987,13 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     if (!FUSED) {
       at(st.t, 4u * (uint32_t)e) = t + 1;
       if (M && (tot || reset_env)) at(tb.drawn, 4u * (uint32_t)e) = drawn + tot;
-      at(out.reward, 4u * (uint32_t)e) = reward_out;
-      at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= KPS(t_end));
+      if (STG) {  // staged: the block writes its envs' rows together (k_step_packed)
+        srew[m.seg] = reward_out;
+        sdone[m.seg] = (uint8_t)(t + 1 >= KPS(t_end));
+      } else {
+        at(out.reward, 4u * (uint32_t)e) = reward_out;
+        at(out.done, (uint32_t)e) = (uint8_t)(t + 1 >= KPS(t_end));
+      }
       if (want_metrics) out.metrics[e] = met;
     }
     if (want_qoe) {
@@ -1054,8 +1059,17 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
                                                              KTables tb, int g0, int ngroups) {
   extern __shared__ int lds_hist[];  // [waves][G][B] when KPS(hist_lds)
   const int lane = threadIdx.x & 63;
-  const int g = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= ngroups) return;
+  const int gb = g0 + block_slot(kp.xcd_remap) * kWavesPerBlock;
+  const int g = gb + (threadIdx.x >> 6);
+  // STG (lean, compile-time U): the block's per-env rows (reward float32, done byte) are
+  // staged in LDS and written together after a barrier -- one 4 NW G-byte reward piece per
+  // block instead of one 4 G-byte piece per wavefront (the rollout kernel's measurement:
+  // such small pieces cost 12 % there); waves without a group only take part in the barrier
+  constexpr bool STG = LEAN && UC != 0 && !PER_ENV_BS;
+  constexpr int GC = UC ? 64 / pitch_of(UC ? UC : 1) : 1;
+  __shared__ float srw[STG ? kWavesPerBlock * GC : 1];
+  __shared__ uint8_t sdn[STG ? kWavesPerBlock * GC : 1];
+  if (!STG && g >= ngroups) return;
   constexpr int PC = UC ? pitch_of(UC) : 0;
   const int U = UC ? UC : kp.U;
   const int P = PC ? PC : kp.U;
@@ -1063,9 +1077,21 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const LaneMap m = lane_map<PC>(lane, P);
   const int e = g * G + m.seg;
   const bool env_ok = (m.seg < G) && (e < kp.E);
-  GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
-  packed_group<PER_ENV_BS, LEAN, UC, false>(kp, st, out, tb, m, a, e, env_ok,
-                                            lds_hist + (threadIdx.x >> 6) * G * kp.B);
+  if (g < ngroups) {
+    GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
+    packed_group<PER_ENV_BS, LEAN, UC, false, 0, 0, STG>(
+        kp, st, out, tb, m, a, e, env_ok, lds_hist + (threadIdx.x >> 6) * G * kp.B, nullptr,
+        nullptr, 0, 1, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
+        sdn + (threadIdx.x >> 6) * GC);
+  }
+  if (STG) {
+    __syncthreads();
+    const int j = (int)threadIdx.x, eo = gb * GC + j;
+    if (j < kWavesPerBlock * GC && eo < kp.E && gb + j / GC < ngroups) {
+      at(out.reward, 4u * (uint32_t)eo) = srw[j];
+      at(out.done, (uint32_t)eo) = sdn[j];
+    }
+  }
 }
 
 // nsteps fused steps per launch (mev_step / mev_rollout with n > 1): each wavefront advances
