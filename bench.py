@@ -8,33 +8,36 @@ Contract (see DESIGN.md "Measurement"):
 
 * One step = one pass of the step over every env on the GPU (BASELINE.json configs[2]:
   65,536 envs of mobile-large-central-v0 per MI355X; weak scaling: each rank owns its own
-  65,536 independent envs, seeds 1000 + global env index). By default steps are issued as
-  ``engine.rollout(40, traj)`` (mev_rollout, two 20-step episodes with the lazy auto-reset
-  between them, as the reference driver loop ``reset(); step() x 20`` repeated): ONE launch of
-  the fused multi-step kernel, which keeps every env's state in registers between the steps
-  and writes EVERY step's outputs (obs, serving, reward, done) to its own row of a
-  [40, E, ...] trajectory buffer in HBM -- the per-step outputs the reference's driver
-  consumes every step (base.py:261) -- bit-identical to 40 one-step launches (--chunk sets
-  the steps per launch; 20 = one episode: ~5 % slower, the launch's fill and drain and the
-  per-group prologue counted over fewer steps). ``--launch single`` issues one-step launches
-  (mev_step(1), outputs overwritten) instead; ``split`` two env halves.
-* Timed region: barrier + synchronize, K steps, the single final all-gather of the
+  65,536 independent envs, seeds 1000 + global env index). Steps are issued as rollout launches
+  of ``--chunk`` steps (default 40 = two 20-step episodes with the lazy auto-reset between
+  them, as the reference driver loop ``reset(); step() x 20`` repeated): ONE launch of the fused
+  multi-step kernel per chunk, which keeps every env's state in registers between its steps and
+  writes EVERY step's outputs (obs, serving, reward, done) to its own row of a trajectory buffer
+  in HBM -- the per-step outputs the reference's driver consumes every step (base.py:261) --
+  bit-identical to one-step launches. Exactly K steps are timed: K // chunk launches of
+  ``chunk`` steps and one launch of the remainder. ``--launch single`` issues one-step
+  launches (mev_step(1), the Gym ``step()``) instead.
+* Warmup: W steps, and then more until ``--warmup-floor-s`` seconds of back-to-back launches
+  have run (untimed; the chip reaches its steady clock -- a 5-step warmup would time a cold
+  launch). ``warmup`` in the line is W as requested; ``warmup_executed`` what ran.
+* Timed region: barrier + synchronize, the K steps, the single final all-gather of the
   (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
   ranks time. Inputs are resident in HBM before timing starts.
-* roofline: algorithmic bytes per launch over the launch's average duration from HIP events
-  on the stream the kernel runs on (around every launch; for one-step launches around every
-  chunk of 20, gaps included). One-step launch: SURVEY.md 8d's per-unit figure, (54*U + 61) B
-  per env-step (canonical: state r+w 34 B/UE + outputs 20 B/UE; per env 61 B), x E. A rollout
-  launch of n steps keeps the env state in registers between its steps, so its algorithmic
-  bytes are every step's outputs, E * n * (20*U + 5), plus the canonical state read and
-  written once, E * (34*U + 56) -- counting the canonical per-step state round trip instead
-  (`canonical_equiv_*`) would put the rate above the HBM peak. The PMC `traffic` is what the
-  launch actually moved.
-  traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
-  (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
+* roofline (the timed launch shape): algorithmic bytes per launch over the launch's average
+  duration from HIP events on the stream the kernel runs on. A rollout launch of n steps keeps
+  the env state in registers between its steps, so its algorithmic bytes are every step's
+  outputs, E * n * (20*U + 5), plus the canonical state read and written once,
+  E * (34*U + 56); SURVEY.md 8d's canonical per-step figure (54*U + 61 B per env-step) counts a
+  state round trip per step that the launch does not make, and would put the rate above the
+  HBM peak (`canonical_equiv_frac`). `traffic`: HBM bytes per launch from the committed
+  rocprofv3 PMC summary (profiles/pmc_traffic.json; FETCH_SIZE x 2 + WRITE_SIZE per the MI355X
+  guide), else null.
+* roofline_step: the one-step launch of ``make().step()`` (mev_step(1)), timed after the timed
+  region (200 launches, HIP events around each), on SURVEY.md 8d's canonical bytes per
+  env-step x E -- the canonical unit of work at its canonical byte count.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
-  per core, run before the GPU is touched.
+  per core of the host share, run before the GPU is touched.
 """
 from __future__ import annotations
 
@@ -51,6 +54,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (whole node), mobile-large-central-v0 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+DTYPE = ("mixed: int16/int32 positions and association, f64 rate and cents, "
+         "f32 obs/utility, int32 fixed-point reward sum")
 
 
 def algorithmic_bytes_per_env_step(num_ues: int, per_env_bs: bool, num_bs: int) -> int:
@@ -60,10 +65,48 @@ def algorithmic_bytes_per_env_step(num_ues: int, per_env_bs: bool, num_bs: int) 
 
 def algorithmic_bytes_rollout(num_ues: int, per_env_bs: bool, num_bs: int, n: int) -> int:
     """Per env, one rollout launch of n steps: every step's outputs (obs 16 B + serving 4 B
-    per UE, reward 4 + done 1 per env; per-env layouts: 8 B per station per step) plus the
-    canonical state read and written once (34 B per UE; PCG64 state r+w 32, inc 16, t r+w 8)."""
-    per_step = 20 * num_ues + 5 + (8 * num_bs if per_env_bs else 0)
-    return n * per_step + 34 * num_ues + 56
+    per UE, reward 4 + done 1 per env) plus the canonical state read and written once (34 B per
+    UE; PCG64 state r+w 32, inc 16, t r+w 8; per-env layouts: the 8 B per station read once)."""
+    per_step = 20 * num_ues + 5
+    return n * per_step + 34 * num_ues + 56 + (8 * num_bs if per_env_bs else 0)
+
+
+def chunk_plan(steps: int, chunk: int):
+    """Launch sizes that add up to exactly `steps`: whole chunks, then the remainder."""
+    chunk = max(1, min(chunk, steps)) if steps > 0 else 1
+    plan = [chunk] * (steps // chunk)
+    if steps % chunk:
+        plan.append(steps % chunk)
+    return plan
+
+
+def timed_run(issue, plan, sync, barrier, make_event, collective):
+    """The timed region: barrier + sync, every launch of `plan` with an event pair around it,
+    the final collective, sync + barrier. Returns (wall seconds, [(start, end, n)])."""
+    events = [(make_event(), make_event(), n) for n in plan]
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for a, b, n in events:
+        a.record()
+        issue(n)
+        b.record()
+    collective()
+    sync()
+    barrier()
+    return time.perf_counter() - t0, events
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """MAX of a float over the ranks of the default group (identity when not distributed)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 # ---------------------------------------------------------------------------------------------
@@ -85,6 +128,19 @@ def _cpu_worker(args):
     return done, time.perf_counter() - t0
 
 
+def host_share_cores() -> int:
+    """Cores of the host share this process may use: its affinity set, capped by the pool's
+    per-GPU CPU share (OMP_NUM_THREADS is set to it on the GPU boxes, 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
 def cpu_baseline(budget_s: float, procs: int):
     from mobile_env.scenarios.registry import LAYOUTS
     lay = LAYOUTS["large"]
@@ -96,10 +152,12 @@ def cpu_baseline(budget_s: float, procs: int):
     wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "host_cpus": os.cpu_count(),
             "sample": (f"oracle/port.py per-object restatement of MComCore.step, "
-                       f"mobile-large-central-v0 (13 BS x 30 UE), {procs} processes x "
-                       f"{budget_s:.0f} s of whole 20-step episodes, seeds 1000+, compute-only "
-                       f"(no JSON dump): {steps} env-steps in {wall:.1f} s")}
+                       f"mobile-large-central-v0 (13 BS x 30 UE), {procs} processes (one per "
+                       f"core of the host share) x {budget_s:.0f} s of whole 20-step episodes, "
+                       f"seeds 1000+, compute-only (no JSON dump): {steps} env-steps in "
+                       f"{wall:.1f} s")}
 
 
 def load_profile(workload: str, envs: int, launch: str = "fused", chunk: int = 40):
@@ -117,11 +175,22 @@ def load_profile(workload: str, envs: int, launch: str = "fused", chunk: int = 4
     return ent.get("hbm_bytes_per_launch"), (avg_ns * 1e-6 if avg_ns else None)
 
 
+def roofline(algo_bytes, launch_ms, traffic):
+    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                             if traffic else None),
+            "algorithmic_bytes_per_launch": algo_bytes, "launch_ms": launch_ms}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--warmup", type=int, default=2000)
+    ap.add_argument("--warmup-floor-s", type=float, default=2.0,
+                    help="untimed warmup continues until this many seconds have run")
     ap.add_argument("--workload", default="mobile-large-central-v0")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -132,9 +201,11 @@ def main():
     ap.add_argument("--chunk", type=int, default=40,
                     help="steps per engine call: per rollout launch (fused), or per C loop of "
                          "one-step launches (single / split); 40 = two episodes")
+    ap.add_argument("--step-launches", type=int, default=200,
+                    help="one-step launches timed after the timed region for roofline_step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
-                    help="minimal run for rocprofv3 (no CPU baseline, no JSON extras)")
+                    help="minimal run for rocprofv3 (no CPU baseline, no step roofline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,8 +216,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.profile_run):
-        procs = max(1, min(16, os.cpu_count() or 1))
-        cpu = cpu_baseline(args.cpu_budget, procs)
+        cpu = cpu_baseline(args.cpu_budget, host_share_cores())
 
     import torch
     import torch.distributed as dist
@@ -173,60 +243,81 @@ def main():
     env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
                           stream_split=2 if args.launch == "split" else 0,
                           fuse_steps=0 if args.launch == "fused" else -1)
+    eng = env.engine
     U, B = env.num_ues, env.num_bs
-    per_env_bs = env.engine.bs_per_env
-    parts = env.engine.launch_parts
+    per_env_bs = eng.bs_per_env
+    parts = eng.launch_parts
     env.reset()
-    CHUNK = args.chunk  # steps per engine call (two 20-step episodes by default)
-    fused = args.launch == "fused" and env.engine.fused_steps
-    traj = env.engine.trajectory(CHUNK) if args.launch == "fused" else None
-
-    def chunk():
-        if traj is not None:
-            env.engine.rollout(CHUNK, traj)  # every step's outputs to its own row
-        else:
-            env.engine.step(CHUNK)
-
-    # warmup (also brings the GPU to its steady clock): the Gym step once, then chunks
-    if args.warmup > 0:
-        env.step()
-        for _ in range(-(-(args.warmup - 1) // CHUNK)):
-            chunk()
-    torch.cuda.synchronize(device)
-
-    # Steps are issued in chunks of CHUNK from C (fused: one rollout launch per chunk; single:
-    # CHUNK back-to-back launches -- a Python call per step would make the host the bottleneck),
-    # with a HIP event pair around every chunk on the caller's stream. With the two-half
-    # launch shape the second half runs on the context's own stream and is joined back
-    # before mev_step returns, so each event pair brackets whole steps of the full batch.
-    K = -(-args.steps // CHUNK) * CHUNK
+    K = args.steps
+    plan = chunk_plan(K, args.chunk)
+    CHUNK = plan[0]
+    fused = args.launch == "fused" and eng.fused_steps
+    traj = eng.trajectory(CHUNK) if args.launch == "fused" else None
     stream = torch.cuda.current_stream(device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K // CHUNK)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        chunk()
-        b.record(stream)
-    if world > 1:  # the one collective: final (reward, done) batch to every rank
-        if traj is not None:  # the last step's row of the trajectory
-            gather_final(traj.reward[CHUNK - 1], traj.done[CHUNK - 1])
-        else:
-            gather_final(env.engine.reward, env.engine.done)
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=device if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def issue(n):
+        if traj is not None:
+            eng.rollout(n, traj)  # every step's outputs to its own row
+        else:
+            eng.step(n)
+
+    # warmup: W steps, then whole chunks until the floor time has passed (steady clock)
+    warm = 0
+    t_w = time.perf_counter()
+    if args.warmup > 0:
+        env.step()  # the Gym surface once
+        warm = 1
+        for n in chunk_plan(args.warmup - 1, CHUNK) if args.warmup > 1 else []:
+            issue(n)
+            warm += n
+        torch.cuda.synchronize(device)
+        while time.perf_counter() - t_w < args.warmup_floor_s:
+            for _ in range(16):
+                issue(CHUNK)
+                warm += CHUNK
+            torch.cuda.synchronize(device)
+    torch.cuda.synchronize(device)
+
+    class _Ev:
+        def __init__(self):
+            self.e = torch.cuda.Event(enable_timing=True)
+
+        def record(self):
+            self.e.record(stream)
+
+    def collective():
+        if world > 1:  # the one collective: final (reward, done) batch to every rank
+            if traj is not None:  # the last step's row of the trajectory
+                gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
+            else:
+                gather_final(eng.reward, eng.done)
+
+    barrier = dist.barrier if world > 1 else (lambda: None)
+    elapsed, events = timed_run(issue, plan, lambda: torch.cuda.synchronize(device), barrier,
+                                _Ev, collective)
+    elapsed = max_over_ranks(elapsed, device)
+    # the launch shape's average duration over the full-size launches (events on the stream)
+    full = [a.e.elapsed_time(b.e) for a, b, n in events if n == CHUNK]
+    chunk_ms = sum(full) / len(full)
+
+    step_roof = None
+    if rank == 0 and fused and not args.profile_run and args.step_launches > 0:
+        # the Gym step() launch (mev_step(1)), canonical bytes, timed after the timed region
+        evs = [(_Ev(), _Ev()) for _ in range(args.step_launches)]
+        for a, b in evs:
+            a.record()
+            eng.step(1)
+            b.record()
+        torch.cuda.synchronize(device)
+        ms = sorted(a.e.elapsed_time(b.e) for a, b in evs)
+        avg = sum(ms) / len(ms)
+        tr1, rp1 = load_profile(args.workload, E, "single")
+        step_roof = roofline(E * algorithmic_bytes_per_env_step(U, per_env_bs, B), avg, tr1)
+        step_roof.update({"median_launch_ms": ms[len(ms) // 2], "launches": len(ms),
+                          "rocprof_launch_ms": rp1,
+                          "env_steps_per_s": E / (avg * 1e-3),
+                          "basis": "SURVEY.md 8d canonical bytes per env-step x E, one-step "
+                                   "launch (make().step(), mev_step(1))"})
 
     if rank == 0:
         value = world * E * K / elapsed
@@ -234,9 +325,20 @@ def main():
         canon_bytes = E * spl * algorithmic_bytes_per_env_step(U, per_env_bs, B)
         algo_bytes = (E * algorithmic_bytes_rollout(U, per_env_bs, B, spl) if fused
                       else canon_bytes)
-        launch_ms = kern_ms * spl
-        achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+        launch_ms = chunk_ms if fused else chunk_ms / CHUNK
         traffic, rocprof_ms = load_profile(args.workload, E, args.launch, CHUNK)
+        roof = roofline(algo_bytes, launch_ms, traffic)
+        roof.update({
+            "canonical_bytes_per_env_step": algorithmic_bytes_per_env_step(U, per_env_bs, B),
+            "canonical_equiv_achieved": canon_bytes / (launch_ms * 1e-3) / 1e9,
+            "canonical_equiv_frac": canon_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "steps_per_launch": spl,
+            "rocprof_launch_ms": rocprof_ms,
+            "launch_shape": (
+                f"fused rollout: {spl} steps per launch, env state in registers between "
+                f"them, every step's outputs to its own trajectory row" if fused else
+                f"{parts} halves per step on {parts} HIP streams" if parts > 1
+                else "one kernel per step")})
         out = {
             "metric": METRIC,
             "value": value,
@@ -244,35 +346,19 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
+            "warmup_executed": warm,
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": DTYPE,
             "data": "synthetic (seeded PCG64 streams, build-defined BS layout)",
             "config": {"workload": args.workload, "envs_per_gpu": E, "global_envs": world * E,
-                       "num_ues": U, "num_bs": B,
+                       "num_ues": U, "num_bs": B, "per_env_layouts": bool(per_env_bs),
+                       "launches": len(plan), "steps_per_launch": CHUNK,
                        "parallelism": f"env-sharded x{world}, no data-path collective"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                          if traffic else None),
-                         "algorithmic_bytes_per_launch": algo_bytes,
-                         "canonical_bytes_per_env_step": algorithmic_bytes_per_env_step(
-                             U, per_env_bs, B),
-                         "canonical_equiv_achieved": canon_bytes / (launch_ms * 1e-3) / 1e9,
-                         "canonical_equiv_frac": (canon_bytes / (launch_ms * 1e-3) / 1e9 /
-                                                  HBM_PEAK_GBS),
-                         "steps_per_launch": spl,
-                         "launch_ms": launch_ms,
-                         "rocprof_launch_ms": rocprof_ms,
-                         "launch_shape": (
-                             f"fused rollout: {spl} steps per launch, env state in registers "
-                             f"between them, every step's outputs to its own trajectory row"
-                             if fused else
-                             f"{parts} halves per step on {parts} HIP streams" if parts > 1
-                             else "one kernel per step")},
+            "roofline": roof,
+            "roofline_step": step_roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 8
+#define MEV_ABI_VERSION 9
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -95,6 +95,15 @@ typedef struct mev_params {
   double util_w1, util_w2, util_w3;               /* coeffs (10, 0, 10) */
   double qoe_low;         /* low-QoE threshold of the layout score (chooseBaseStation.ipynb
                              cell 5: low_qoe_threshold = 0.0) */
+  /* Channel rate table (optional, HOST memory, read by mev_create only): rate_table[d2] =
+   * Channel.datarate(bs, ue, Channel.calculateSNR(bs, ue)) for a pair at integer squared
+   * distance d2 (channels.py:24-27,78-83,133-146), for d2 in [0, rate_table_len); the pairs at
+   * d2 >= rate_table_len are not connectable (snr <= snr_tr). The Python host builds it with
+   * numpy in the reference's operation order (mobile_env.core.channels), which makes it the
+   * reference's own values on the host that runs it. NULL: mev_create builds it on the host
+   * with the C library's log10 / pow / log2 in the same order (mev_build_rate_table). */
+  const double* rate_table;
+  int64_t rate_table_len;
 } mev_params;
 
 typedef struct mev_state {
@@ -124,12 +133,12 @@ typedef struct mev_ctx mev_ctx;
 /* Library ABI version (MEV_ABI_VERSION). */
 int mev_abi_version(void);
 
-/* Build a context on the current HIP device: validates params and builds, ON THE
- * DEVICE, the channel table (Okumura-Hata -> SNR -> Shannon rate at every integer
- * squared distance, channels.py:24-27,78-83,133-146; replaces the per-pair
- * Channel.calculateSNR/datarate calls of base.py:212-214,427-431) and the PCG64
- * jump-ahead table. Replaces MComCore.__init__'s plugin construction
- * (base.py:57-61). Synchronous. */
+/* Build a context on the current HIP device: validates params, uploads the channel table
+ * (Okumura-Hata -> SNR -> Shannon rate at every integer squared distance,
+ * channels.py:24-27,78-83,133-146; replaces the per-pair Channel.calculateSNR/datarate calls
+ * of base.py:212-214,427-431; params->rate_table, or built on the host) and builds the PCG64
+ * jump-ahead table. Replaces MComCore.__init__'s plugin construction (base.py:57-61).
+ * Synchronous. */
 int mev_create(const mev_params* params, mev_ctx** out);
 void mev_destroy(mev_ctx* ctx);
 
@@ -145,6 +154,28 @@ const double* mev_rate_table(const mev_ctx* ctx);
 /* Copy the first n entries of the channel rate table to dst (host or device memory,
  * hipMemcpyDefault). Synchronous. */
 int mev_copy_rate_table(const mev_ctx* ctx, double* dst, int64_t n);
+
+/* Host: the channel rate table of params' bs_* / ue_* values with the C library's float64
+ * log10 / pow / log2 in the reference's operation order (OkumuraHata.power_loss
+ * channels.py:133-146, calculateSNR channels.py:24-27, datarate channels.py:78-83; the
+ * distance is sqrt(d2), correctly rounded, like shapely's). Returns n = d2max + 1 (the
+ * connectable squared distances are exactly [0, n)) and writes min(n, cap) entries to dst
+ * (may be NULL with cap 0: query); MEV_ECHANNEL if connectivity is not a prefix of d2.
+ * numpy's log10 (SIMD loops on AVX-512 hosts) can differ from the C library's by one ulp
+ * on a few d2: the Python host passes numpy's table in params->rate_table instead. */
+int64_t mev_build_rate_table(const mev_params* params, double* dst, int64_t cap);
+
+/* Diagnostic (tests): the device's rounded ResourceFair shares, cents(n, d2) =
+ * rint((rate_full[d2] / n) * 100) as the step kernels compute them (base.py:427-435,
+ * schedules.py:20-22), for n in [1, nmax] and d2 in [0, d2max]: dst is a DEVICE buffer
+ * [nmax][d2max + 1] of float64. path 0: the reciprocal form (one-step and block kernels),
+ * path 1: the 100/n table form (n <= 64, LDS-table rollouts). Stream-ordered. */
+int mev_share_cents(const mev_ctx* ctx, int32_t nmax, int32_t path, double* dst, void* stream);
+
+/* The rollout kernel instance mev_rollout runs for this context: 0 generic, s > 0 the
+ * registered scenario s compiled with its parameters as constants (chosen when every value
+ * matches; MEV_SCN=0 in the environment at mev_create forces the generic instance). */
+int mev_rollout_instance(const mev_ctx* ctx);
 
 /* Host helper: numpy-compatible seeding, np.random.default_rng(seed) ->
  * SeedSequence(seed) -> PCG64 (movement seed = config seed + 4, base.py:156-168).

@@ -51,6 +51,8 @@ namespace {
 
 constexpr int kMaxU = 1024;
 constexpr int kMaxB = 1024;
+// largest squared distance of a UE (inside the map) to a station (coordinates < 1024)
+constexpr int64_t kD2Top = 2 * 1023 * 1023;
 constexpr int kKeyBits = 10;
 // (d2, bs) association key: BS index in the low kKeyBits bits
 
@@ -573,35 +575,32 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uin
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
-// The stores of a Pending step into row `row` of the output buffers (row 0 and nrows 1 when
-// the outputs are overwritten every step), branch-free: raw buffer stores over the whole
-// trajectory (loop-invariant descriptors; nrows * row bytes < 2^32, checked by the host) whose
-// lanes without data (padding lanes; non-leaders for the per-env rows) take the offset one
-// past the end, which the buffer range check drops. Without branches every path issues the
-// same VMEM ops, so the compiler's wait for the next gather can leave these stores in flight.
+// The stores of a Pending step into row `row` of the output buffers (row 0 when the outputs
+// are overwritten every step), branch-free: raw buffer stores through one descriptor per row
+// (its base moves with the row, so a trajectory of any length needs no 32-bit offset range),
+// whose lanes without data (padding lanes; non-leaders for the per-env rows) take the offset
+// one past the row's end, which the buffer range check drops. Without branches every path
+// issues the same VMEM ops, so the compiler's wait for the next gather can leave these stores
+// in flight. The scalar offset stays the constant 0: with an SGPR soffset LLVM omits the wait
+// state between a > 8-byte buffer store and a VALU write of its data registers, and on gfx950
+// that write then corrupts the stored data (seen as other values in a few obs rows;
+// tools/check_store_hazard.py checks the generated assembly for such stores).
 template <bool LEAN, bool SMALL = true>
 __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p, uint32_t E,
-                                              uint32_t EU, uint32_t row, uint32_t nrows) {
+                                              uint32_t EU, uint32_t row) {
   const uint32_t robs = 16u * EU, rsrv = 4u * EU, rrew = 4u * E;  // row bytes
-  const uint32_t nobs = nrows * robs, nsrv = nrows * rsrv, nrew = nrows * rrew,
-                 ndone = nrows * E;
   const v4u32 ob = {__float_as_uint(p.obs.x), __float_as_uint(p.obs.y),
                     __float_as_uint(p.obs.z), __float_as_uint(p.obs.w)};
-  // lane part of the offset (loop-invariant; one past the end for lanes without data: the
-  // buffer range check drops those, as voffset + soffset < 2^32 -- nrows * row bytes < 2^31)
-  // + the row as the scalar offset
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving, nsrv),
-                                        p.valid ? 4u * p.ui : nsrv, row * rsrv, 0);
-  // (the 16-byte store takes its row in voffset: with an SGPR soffset the compiler omits the
-  // wait state between a > 8-byte store and a VALU write of its data registers, and on gfx950
-  // that write then corrupts the stored data -- seen as other values in a few obs rows)
-  __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs, nobs),
-                                         (p.valid ? 16u * p.ui : nobs) + row * robs, 0, 0);
+  const size_t ru = (size_t)row * EU, re = (size_t)row * E;
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving + ru, rsrv),
+                                        p.valid ? 4u * p.ui : rsrv, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs + ru, robs),
+                                         p.valid ? 16u * p.ui : robs, 0, 0);
   if (SMALL) {  // (else staged in LDS by the caller: k_steps_packed, STG)
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward, nrew),
-                                          p.lead ? 4u * (uint32_t)p.e : nrew, row * rrew, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done, ndone),
-                                         p.lead ? (uint32_t)p.e : ndone, row * E, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward + re, rrew),
+                                          p.lead ? 4u * (uint32_t)p.e : rrew, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)p.done, out_rsrc(out.done + re, E),
+                                         p.lead ? (uint32_t)p.e : E, 0, 0);
   }
   if (!LEAN) {
     const KOut o = out_row(out, (int)E, (int)(EU / E), (int)row);
@@ -622,7 +621,7 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //   FUSED: one of several steps of a launch (mev_step(n), n > 1): the env state stays in
 //         registers between the steps (`cur` is updated; the caller stores it after the last
 //         step), the per-step outputs are written every step as in separate launches.
-//   FUSED steps write row `row` of `nrows` output rows (`out` is the base, row 0); without
+//   FUSED steps write row `row` of the output rows (`out` is the base, row 0); without
 //   LDSA they defer their stores (Pending): `pend` holds the previous step's outputs (for row
 //   row - 1; nothing valid before the first step) and receives this step's.
 //   LDSM: (fused, shared layout) association from the LDS copy of the compact tables at
@@ -637,7 +636,6 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              bool env_ok, int* __restrict__ hist,
                                              const int* __restrict__ ltab = nullptr,
                                              Pending* pend = nullptr, int row = 0,
-                                             int nrows = 1,
                                              const char* __restrict__ lblob = nullptr,
                                              u128* __restrict__ lpcg = nullptr,
                                              float* __restrict__ srew = nullptr,
@@ -872,7 +870,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   constexpr bool DEFER = FUSED && !LDSA;
   if (DEFER) {
     flush_pending<LEAN>(out, *pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
-                        (uint32_t)max(row - 1, 0), (uint32_t)nrows);
+                        (uint32_t)max(row - 1, 0));
     asm volatile("" ::"v"(srv), "v"(full));
   }
 
@@ -963,8 +961,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     up.lead = up.done = false;
     up.e = 0;
     up.reward = 0.f;
-    flush_pending<LEAN, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
-                               (uint32_t)nrows);
+    flush_pending<LEAN, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
   }
   const bool lead = env_ok && leader;
   float reward_out = 0.f;
@@ -1022,8 +1019,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       *pend = cp;
     } else {
       if (!STG)
-        flush_pending<LEAN>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row,
-                            (uint32_t)nrows);
+        flush_pending<LEAN>(out, cp, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
       if (STG && lead) {  // this step's row slot of the workgroup's staged per-env rows
         srew[m.seg] = reward_out;
         sdone[m.seg] = (uint8_t)cp.done;
@@ -1081,7 +1077,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
     GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
     packed_group<PER_ENV_BS, LEAN, UC, false, 0, 0, STG>(
         kp, st, out, tb, m, a, e, env_ok, lds_hist + (threadIdx.x >> 6) * G * kp.B, nullptr,
-        nullptr, 0, 1, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
+        nullptr, 0, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
         sdn + (threadIdx.x >> 6) * GC);
   }
   if (STG) {
@@ -1114,9 +1110,10 @@ __device__ __forceinline__ void flush_staged(const KOut& out, const float* srew,
   for (int q = threadIdx.x; q < nr * NWG; q += NT) {
     const int r = q / NWG, j = q - r * NWG;
     if (e0 + j < E) {
-      const uint32_t o = (uint32_t)(row0 + r) * (uint32_t)E + (uint32_t)(e0 + j);
-      at(out.reward, 4u * o) = srew[q];
-      at(out.done, o) = sdone[q];
+      const size_t ro = (size_t)(row0 + r) * (size_t)E;
+      const uint32_t o = (uint32_t)(e0 + j);
+      at(out.reward + ro, 4u * o) = srew[q];
+      at(out.done + ro, o) = sdone[q];
     }
   }
   __syncthreads();
@@ -1210,19 +1207,18 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     // the group's inputs have landed before the loop: otherwise the compiler's wait for them,
     // merged into the loop header, would also wait for the previous step's stores
     __builtin_amdgcn_s_waitcnt(0);
-    const int nrows = traj ? nsteps : 1;
     const uint64_t envok_w = bal(env_ok), valid_w = bal(env_ok && m.u < U);
     for (int i = 0; i < nsteps; ++i) {
       const int sr = STG ? i % stage_rows : 0;
       moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG>(
-          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, nrows, lblob, lpcg,
+          kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, lblob, lpcg,
           srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w);
       if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
         flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1);
     }
     if (!LDSA)  // the last step's deferred outputs
       flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
-                          traj ? (uint32_t)(nsteps - 1) : 0u, (uint32_t)nrows);
+                          traj ? (uint32_t)(nsteps - 1) : 0u);
     // the state after the last step
     if (env_ok && m.u < U)
       store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
@@ -1492,29 +1488,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 // ------------------------------------------------------------------------------------
 // Table builders (run once per context, on the device)
 // ------------------------------------------------------------------------------------
-struct ChanParams {
-  double bw, freq, tx, hb, hu, noise, snr_tr;
-};
-
-// Channel.calculateSNR + Channel.datarate at integer squared distance d2
-// (channels.py:24-27,78-83; OkumuraHata.power_loss channels.py:133-146, same op order).
-__global__ void k_channel_table(ChanParams c, int d2_hi, double* __restrict__ rate,
-                                int* __restrict__ d2max_out, int* __restrict__ count_out) {
-  const int d2 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d2 > d2_hi) return;
-  const double distance = sqrt((double)d2);
-  const double ch = 0.8 + (1.1 * log10(c.freq) - 0.7) * c.hu - 1.56 * log10(c.freq);
-  const double tmp_1 = 69.55 - ch + 26.16 * log10(c.freq) - 13.82 * log10(c.hb);
-  const double tmp_2 = 44.9 - 6.55 * log10(c.hb);
-  const double loss = tmp_1 + tmp_2 * log10(distance + 1e-16);
-  const double power = pow(10.0, (c.tx - loss) / 10.0);
-  const double snr = power / c.noise;
-  const bool conn = snr > c.snr_tr;
-  rate[d2] = conn ? c.bw * log2(1.0 + snr) : 0.0;
-  if (conn) {
-    atomicMax(d2max_out, d2);
-    atomicAdd(count_out, 1);
-  }
+// Rounded ResourceFair shares as the step kernels form them (mev_share_cents, tests):
+// cents[n - 1][d2] for n in [1, nmax]; path 1 uses the 100/n table form of the LDS rollouts.
+__global__ void k_share_cents(const double* __restrict__ rate_full, int d2n, int nmax, int path,
+                              double* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)d2n * nmax) return;
+  const int n = (int)(i / d2n) + 1, d2 = (int)(i - (int64_t)(n - 1) * d2n);
+  float cf;
+  dst[i] = path ? share_cents_r(rate_full[d2], 100.0 / (double)n, n, cf)
+                : share_cents(rate_full[d2], n, cf);
 }
 
 // Scaled-utility table over rounded rates: tab[k] = scaled_utility(k / 100), evaluated by
@@ -1653,6 +1636,7 @@ struct mev_ctx {
   int* drawn;
   hipStream_t aux;    // second stream of the two-half shape
   hipEvent_t ev_fork, ev_join;
+  int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -1695,6 +1679,8 @@ static int validate(const mev_params* p) {
   if ((int64_t)p->num_envs * p->num_ues >= ((int64_t)1 << 28)) return MEV_EINVAL;
   if (!(p->velocity >= 0.0) || !(p->ue_noise > 0.0) || !(p->util_upper > p->util_lower))
     return MEV_EINVAL;
+  if (p->rate_table && (p->rate_table_len < 0 || p->rate_table_len > kD2Top + 1))
+    return MEV_EINVAL;
   return MEV_OK;
 }
 
@@ -1708,9 +1694,9 @@ static unsigned fbits(float f) {
   memcpy(&u, &f, 4);
   return u;
 }
-static int match_scn(const KParams& kp) {
-  static const char* sw = getenv("MEV_SCN");  // dev A/B switch: 0 = always the generic kernel
-  if (sw && atoi(sw) == 0) return 0;
+static int match_scn(const mev_ctx* ctx) {
+  if (!ctx->scn_allowed) return 0;
+  const KParams& kp = ctx->kp;
   for (int s = 1; s <= 2; ++s) {
     const ScnConst c = scn_const(s);
     if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
@@ -1754,7 +1740,7 @@ static int build_lds_tables(mev_ctx* c) {
   kp.lds_mode = 0;
   const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 force a mode
   const int want = sw ? atoi(sw) : 2;
-  if (want == 0 || c->p.bs_per_env || kp.B > 15 || kp.U > 64) return MEV_OK;
+  if (want == 0 || c->p.bs_per_env || kp.B > 15 || kp.U > 64 || c->d2max < 0) return MEV_OK;
   const int cells = kp.W * kp.H;
   const int d2max = c->d2max;
   const size_t nwords = (size_t)d2max / 32 + 1;
@@ -1850,6 +1836,41 @@ static int build_lds_tables(mev_ctx* c) {
   return MEV_OK;
 }
 
+// Channel.calculateSNR + Channel.datarate at integer squared distance d2 on the host, float64,
+// the reference's operation order (OkumuraHata.power_loss channels.py:133-146: shapely's
+// distance = sqrt(d2); calculateSNR channels.py:24-27; datarate channels.py:78-83).
+static double host_snr(const mev_params* p, int64_t d2) {
+  const double distance = sqrt((double)d2);
+  const double f = p->bs_freq, hb = p->bs_height, hu = p->ue_height;
+  const double ch = 0.8 + (1.1 * log10(f) - 0.7) * hu - 1.56 * log10(f);
+  const double tmp_1 = 69.55 - ch + 26.16 * log10(f) - 13.82 * log10(hb);
+  const double tmp_2 = 44.9 - 6.55 * log10(hb);
+  const double loss = tmp_1 + tmp_2 * log10(distance + 1e-16);
+  const double power = pow(10.0, (p->bs_tx - loss) / 10.0);
+  return power / p->ue_noise;
+}
+
+int64_t mev_build_rate_table(const mev_params* p, double* dst, int64_t cap) {
+  if (!p || cap < 0 || (cap > 0 && !dst)) return MEV_EINVAL;
+  if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
+  // connectable d2 = a prefix [0, n): scanned over the map's squared distances, and over every
+  // station distance (coordinates < 1024) when the whole map range connects
+  const int64_t map_hi = (int64_t)(p->width - 1) * (p->width - 1) +
+                         (int64_t)(p->height - 1) * (p->height - 1);
+  int64_t n = 0;
+  bool prefix = true;
+  for (int64_t d2 = 0; d2 <= kD2Top; ++d2) {
+    if (d2 > map_hi && n <= map_hi) break;  // the map's range decided it
+    const double snr = host_snr(p, d2);
+    if (snr > p->ue_snr_tr) {
+      if (n != d2) prefix = false;
+      if (d2 < cap) dst[d2] = p->bs_bw * log2(1.0 + snr);
+      n = d2 + 1;
+    }
+  }
+  return prefix ? n : MEV_ECHANNEL;
+}
+
 int mev_create(const mev_params* params, mev_ctx** out) {
   if (!out) return MEV_EINVAL;
   *out = nullptr;
@@ -1924,31 +1945,34 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     }
   }
 
-  // ---- channel table on the device ----
-  const int d2_hi = (params->width - 1) * (params->width - 1) +
-                    (params->height - 1) * (params->height - 1);
-  int* d_aux = nullptr;
-  if (hipMalloc(&c->rate_full, sizeof(double) * (size_t)(d2_hi + 1)) != hipSuccess ||
-      hipMalloc(&d_aux, 2 * sizeof(int)) != hipSuccess) {
-    if (d_aux) (void)hipFree(d_aux);
-    mev_destroy(c);
-    return MEV_ENOMEM;
+  // ---- channel table: the caller's (numpy, Python host), else built here with libm ----
+  {
+    std::vector<double> host;
+    const double* tab = params->rate_table;
+    int64_t n = params->rate_table_len;
+    if (tab == nullptr) {
+      n = mev_build_rate_table(params, nullptr, 0);
+      if (n < 0) {
+        mev_destroy(c);
+        return (int)n;
+      }
+      host.resize((size_t)std::max<int64_t>(n, 1));
+      (void)mev_build_rate_table(params, host.data(), n);
+      tab = host.data();
+    }
+    c->d2max = (int)n - 1;
+    c->kp.d2max = c->d2max;
+    // (one entry at least: lanes without a server read entry 0 unconditionally)
+    if (hipMalloc(&c->rate_full, sizeof(double) * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) {
+      mev_destroy(c);
+      return MEV_ENOMEM;
+    }
+    MEV_HIP(hipMemset(c->rate_full, 0, sizeof(double)));
+    if (n > 0) MEV_HIP(hipMemcpy(c->rate_full, tab, sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
   }
-  const int init_aux[2] = {-1, 0};
-  MEV_HIP(hipMemcpy(d_aux, init_aux, sizeof(init_aux), hipMemcpyHostToDevice));
-  ChanParams cp{params->bs_bw, params->bs_freq, params->bs_tx, params->bs_height,
-                params->ue_height, params->ue_noise, params->ue_snr_tr};
-  hipLaunchKernelGGL(k_channel_table, dim3((d2_hi + 256) / 256), dim3(256), 0, 0, cp, d2_hi,
-                     c->rate_full, d_aux, d_aux + 1);
-  MEV_HIP(hipGetLastError());
-  int aux[2];
-  MEV_HIP(hipMemcpy(aux, d_aux, sizeof(aux), hipMemcpyDeviceToHost));
-  MEV_HIP(hipFree(d_aux));
-  c->d2max = aux[0];
-  c->kp.d2max = c->d2max;
-  if (aux[1] != aux[0] + 1) {  // connectable set must be exactly [0, d2max]
-    mev_destroy(c);
-    return MEV_ECHANNEL;
+  {
+    const char* sw = getenv("MEV_SCN");  // dev A/B switch: 0 = always the generic rollout kernel
+    c->scn_allowed = !(sw && atoi(sw) == 0);
   }
 
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
@@ -2061,6 +2085,25 @@ int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EI
 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 
+int mev_rollout_instance(const mev_ctx* c) {
+  if (!c) return MEV_EINVAL;
+  const bool lean_ok = !c->kp.util_direct;
+  return (c->kp.lds_assoc > 0 && c->kp.lds_mode == 2 && !c->p.bs_per_env && lean_ok)
+             ? match_scn(c) : 0;
+}
+
+int mev_share_cents(const mev_ctx* c, int32_t nmax, int32_t path, double* dst, void* stream) {
+  if (!c || !dst || nmax < 1 || nmax > kMaxU || path < 0 || path > 1) return MEV_EINVAL;
+  if (path == 1 && nmax > 64) return MEV_EINVAL;
+  const int d2n = c->d2max + 1;
+  if (d2n <= 0) return MEV_OK;
+  const int64_t total = (int64_t)d2n * nmax;
+  hipLaunchKernelGGL(k_share_cents, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, c->rate_full, d2n, nmax, (int)path, dst);
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
 int mev_copy_rate_table(const mev_ctx* c, double* dst, int64_t n) {
   if (!c || !dst || n < 0 || n > (int64_t)c->d2max + 1) return MEV_EINVAL;
   MEV_HIP(hipMemcpy(dst, c->rate_full, sizeof(double) * (size_t)n, hipMemcpyDefault));
@@ -2146,7 +2189,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const int ldsm = ldsa ? kp.lds_mode : 0;
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
     if (ldsm == 2 && lean) {  // a registered scenario's constants (scn_const)
-      const int scn = match_scn(kp);
+      const int scn = match_scn(c);
       if (scn == 1) kf = k_steps_packed<false, true, 15, 2, 1>;
       if (scn == 2) kf = k_steps_packed<false, true, 30, 2, 2>;
     }
@@ -2155,17 +2198,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
     size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
     const bool stg = ldsm == 2 && lean && stages(kp);  // k_steps_packed STG
-    // trajectory rows per launch: the kernel's buffer descriptors span nrows rows (< 2^31 B,
-    // flush_pending)
-    const int64_t row_bytes = 16 * (int64_t)kp.E * kp.U;
-    const int rows_max = traj ? (int)std::max<int64_t>(1, 0x7FFFFFFFll / row_bytes) : nsteps;
-    for (int i0 = 0; i0 < nsteps; i0 += rows_max) {
-      const int n = std::min(rows_max, nsteps - i0);
-      const int srows = stg ? std::min(c->stage_rows, n) : 1;
-      kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
-           stream>>>(kp, ks, traj ? out_row(ko, kp.E, kp.U, i0) : ko, tb, groups, n,
-                     traj ? 1 : 0, srows);
-    }
+    const int srows = stg ? std::min(c->stage_rows, nsteps) : 1;
+    kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
+         stream>>>(kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -24,7 +24,8 @@ MEV_ECHANNEL = -1001
 # every symbol include/mev.h declares (tests check the library exports all of them)
 EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_lds_tables_bytes",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
-           "mev_update_stations",
+           "mev_update_stations", "mev_build_rate_table", "mev_share_cents",
+           "mev_rollout_instance",
            "mev_reset", "mev_prepare_draws", "mev_step", "mev_rollout", "mev_strerror", "mev_last_hip_error")
 
 
@@ -43,6 +44,7 @@ class MevParams(C.Structure):
         ("util_lower", C.c_double), ("util_upper", C.c_double),
         ("util_w1", C.c_double), ("util_w2", C.c_double), ("util_w3", C.c_double),
         ("qoe_low", C.c_double),
+        ("rate_table", C.c_void_p), ("rate_table_len", C.c_int64),
     ]
 
 
@@ -113,6 +115,12 @@ def lib():
         L.mev_rollout.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),
                                   C.c_int32, C.c_void_p]
         L.mev_rollout.restype = C.c_int
+        L.mev_build_rate_table.argtypes = [C.POINTER(MevParams), C.c_void_p, C.c_int64]
+        L.mev_build_rate_table.restype = C.c_int64
+        L.mev_share_cents.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.mev_share_cents.restype = C.c_int
+        L.mev_rollout_instance.argtypes = [C.c_void_p]
+        L.mev_rollout_instance.restype = C.c_int
         L.mev_strerror.argtypes = [C.c_int]
         L.mev_strerror.restype = C.c_char_p
         L.mev_last_hip_error.restype = C.c_char_p

@@ -5,15 +5,20 @@ Plugins here are lowered to device constants by the engine (see ``lower``); the 
 """
 from __future__ import annotations
 
+import numpy as np
+
 
 class Arrival:
     def __init__(self, ep_time: int, seed: int, reset_rng_episode: bool, **kwargs):
         self.ep_time = ep_time
         self.seed = seed
         self.reset_rng_episode = reset_rng_episode
+        self.rng = None
 
     def reset(self) -> None:
-        """No RNG is consumed by the built-in arrival model (arrival.py:15-17 seeds one)."""
+        """arrival.py:15-17 (the built-in NoDeparture draws nothing from it)."""
+        if self.reset_rng_episode or self.rng is None:
+            self.rng = np.random.default_rng(self.seed)
 
     def setArrivalTime(self, ue) -> int:
         raise NotImplementedError

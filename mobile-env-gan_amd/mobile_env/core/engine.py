@@ -57,8 +57,19 @@ class EngineParams:
     fuse_steps: int = 0    # mev_params.fuse_steps: 0 step(n > 1) in one launch, -1 n launches
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
 
-    def to_c(self, bs_per_env: bool) -> N.MevParams:
+    def rate_table(self):
+        """The channel rate table of these parameters (numpy, reference op order; see
+        mobile_env.core.channels): float64 [d2max + 1]."""
+        from .channels import OkumuraHata
+        return OkumuraHata().rate_table(self.bs, self.ue, int(self.width), int(self.height))
+
+    def to_c(self, bs_per_env: bool, rate_table=None) -> N.MevParams:
+        """mev_params; ``rate_table`` (float64 numpy array, kept alive by the caller until
+        mev_create returns) is passed as mev_params.rate_table."""
+        tab = (C.c_void_p(rate_table.ctypes.data), len(rate_table)) if rate_table is not None \
+            else (C.c_void_p(None), 0)
         return N.MevParams(
+            rate_table=tab[0], rate_table_len=tab[1],
             num_envs=self.num_envs, num_ues=self.num_ues, num_bs=self.num_bs,
             width=int(self.width), height=int(self.height), ep_max_time=int(self.ep_max_time),
             arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
@@ -145,9 +156,11 @@ class StepEngine:
         _check_station_range(bs, bs_count)
         L = N.lib()
         with torch.cuda.device(device):
-            cp = params.to_c(self.bs_per_env)
+            tab = params.rate_table()  # the reference's own values (numpy, host)
+            cp = params.to_c(self.bs_per_env, tab)
             ctx = C.c_void_p()
             N.check(L.mev_create(C.byref(cp), C.byref(ctx)), "mev_create")
+            del tab
             self._ctx = ctx
             self._lib = L
             kw = dict(device=device)
@@ -215,8 +228,23 @@ class StepEngine:
         """Bytes of the LDS association tables of rollout launches (0: L2 map gather)."""
         return int(self._lib.mev_lds_tables_bytes(self._ctx))
 
+    @property
+    def rollout_instance(self) -> int:
+        """Rollout kernel instance: 0 generic, s > 0 registered scenario s with constants."""
+        return int(self._lib.mev_rollout_instance(self._ctx))
+
+    def share_cents(self, nmax: int, path: int = 0):
+        """Device rounded shares rint((rate_full[d2] / n) * 100) for n in [1, nmax] as the
+        kernels form them (path 0: reciprocal form; 1: 100/n table form, nmax <= 64):
+        float64 [nmax, d2max + 1] on the device (tests)."""
+        out = torch.empty((int(nmax), self.d2max + 1), dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_share_cents(self._ctx, int(nmax), int(path), _ptr(out),
+                                              self._stream()), "mev_share_cents")
+        return out
+
     def rate_table(self):
-        """Host copy (numpy float64) of the device-built channel table rate_full[0..d2max]."""
+        """Host copy (numpy float64) of the device channel table rate_full[0..d2max]."""
         import numpy as np
         host = np.zeros(self.d2max + 1, dtype=np.float64)
         N.check(self._lib.mev_copy_rate_table(self._ctx, host.ctypes.data, len(host)),

@@ -7,6 +7,8 @@ else raises ``NotImplementedError`` (there is no CPU path to fall back to).
 """
 from __future__ import annotations
 
+from inspect import getattr_static
+
 from .arrival import NoDeparture
 from .channels import OkumuraHata
 from .engine import EngineParams
@@ -23,14 +25,34 @@ _BUILTIN = {
 }
 
 
+# the methods whose semantics the kernels implement, per plugin: a subclass of a built-in class
+# that overrides none of them lowers like the built-in (the reference instantiates whatever
+# class the config names, base.py:57-61); one that overrides any has no kernel
+_KERNEL_METHODS = {
+    "arrival": ("setArrivalTime", "setDepartureTime"),
+    "channel": ("power_loss", "calculateSNR", "datarate", "snr_of_distance", "rate_table",
+                "_loss", "_snr_table"),
+    "scheduler": ("share",),
+    "movement": ("move", "initial_position", "reset", "_draw"),
+    "utility": ("calculateUtility", "scaleUtility", "unscaleUtility"),
+}
+
+
 def check_plugins(arrival, channel, scheduler, movement, utility):
     for key, obj in (("arrival", arrival), ("channel", channel), ("scheduler", scheduler),
                      ("movement", movement), ("utility", utility)):
         want = _BUILTIN[key]
-        if type(obj) is not want:
+        if not isinstance(obj, want):
             raise NotImplementedError(
                 f"{key} plugin {type(obj).__name__} has no device kernel; the MI355X engine "
                 f"implements {want.__name__} (reference default, base.py:112-116)")
+        changed = [m for m in _KERNEL_METHODS[key]
+                   if getattr_static(type(obj), m, None) is not getattr_static(want, m, None)]
+        if changed:
+            raise NotImplementedError(
+                f"{key} plugin {type(obj).__name__} overrides {', '.join(changed)} of "
+                f"{want.__name__}: the device kernel implements {want.__name__}'s semantics "
+                f"only")
 
 
 def _uniform(values, what):

@@ -1,12 +1,14 @@
 """Utility plugins (reference core/utilities.py:7-58).
 
 ``BoundedLogUtility`` (clip(w1 ln(w2 + r) / ln(w3), lower, upper), scaled to [-1, 1]) runs
-inside the step kernel. ``scaleUtility``/``unscaleUtility`` are the plain affine maps of
-the reference (used by host bookkeeping, e.g. the idle value of a station).
+inside the step kernel. The per-value methods are the reference's (numpy scalars) for callers
+that use the plugin directly and for host bookkeeping (e.g. the idle value of a station).
 """
 from __future__ import annotations
 
 from typing import Tuple
+
+import numpy as np
 
 
 class Utility:
@@ -17,7 +19,7 @@ class Utility:
         pass
 
     def calculateUtility(self, datarate) -> float:
-        raise NotImplementedError("utilities are evaluated on the GPU by libmev")
+        raise NotImplementedError(f"{type(self).__name__} defines no calculateUtility")
 
     def scaleUtility(self, utility) -> float:
         raise NotImplementedError
@@ -37,6 +39,13 @@ class BoundedLogUtility(Utility):
         self.lower = lower
         self.upper = upper
         self.coeffs = coeffs
+
+    def calculateUtility(self, datarate) -> float:
+        """utilities.py:44-53: lower for a non-positive rate, else the clipped log utility."""
+        w1, w2, w3 = self.coeffs
+        if datarate <= 0.0:
+            return self.lower
+        return np.clip(w1 * np.log(w2 + datarate) / np.log(w3), self.lower, self.upper)
 
     def scaleUtility(self, utility) -> float:
         return 2 * (utility - self.lower) / (self.upper - self.lower) - 1

@@ -13,7 +13,7 @@ stub modules for its render-only / geometry dependencies that are absent from th
 * ``svgpath2mpl``       -- BS glyph for rendering only (reference util.py:4,24)
 
 The per-step JSON dump of the reference (base.py:261,298-349) is disabled and the process runs
-from a scratch directory. Usage:  python tests/golden/make_golden.py
+from a scratch directory. Usage:  python tests/golden/make_golden.py [--extra]
 """
 from __future__ import annotations
 
@@ -176,6 +176,84 @@ def rate_table(OkumuraHata, bs_params, ue_params, d2_hi):
     return snr, rate
 
 
+def _build_mixed(ref_base, BaseStation, UserEquipment, bs_xy, bs_params, ue_params, seed):
+    """FixedCore over stations / UEs that each carry their OWN parameters (entities.py:7-22,
+    33-45): bs_params / ue_params are lists of kwargs per entity."""
+    build = _make_fixed_core(ref_base, BaseStation, UserEquipment)
+    env, _ = build(bs_xy, len(ue_params), seed)  # for the FixedCore class and config
+    stations = [BaseStation(i, (int(x), int(y)), **bs_params[i]) for i, (x, y) in enumerate(bs_xy)]
+    users = [UserEquipment(i, **ue_params[i]) for i in range(len(ue_params))]
+    return type(env)(stations, users, {"seed": seed}), users
+
+
+def extra_fixtures(ref_base, BaseStation, UserEquipment):
+    """Round-2 fixtures: per-env 128-station layouts at 1024 UEs (the layout mode of
+    mobile-custom-128x1024-v0), and heterogeneous per-station / per-UE parameters."""
+    out = {}
+    build = _make_fixed_core(ref_base, BaseStation, UserEquipment)
+    # -- per-env 128 x 1024: 3 envs, each its own uniform-integer layout (the registry's
+    #    synthetic layouts: torch.Generator seeded with the env seed, randint(0, 200)), 3 steps
+    import torch
+    seeds = [2024, 2025, 2026]
+    lays, runs = [], []
+    for sd in seeds:
+        g = torch.Generator()
+        g.manual_seed(sd)
+        bs = torch.randint(0, 200, (128, 2), generator=g, dtype=torch.int32).numpy()
+        env, users = build(bs.tolist(), 1024, sd, ue_params={"velocity": 10})
+        env.reset()
+        init = [[int(ue.x), int(ue.y)] for ue in users]
+        recs = []
+        for s in range(3):
+            env.step(0, s)
+            recs.append(_record_step(env, users))
+        lays.append(bs)
+        runs.append((init, recs))
+        print("custom128x1024_perenv seed", sd)
+    out["custom128x1024_perenv"] = dict(
+        bs_xy=np.asarray(lays, dtype=np.int64), seeds=np.asarray(seeds), velocity=np.float64(10),
+        init_xy=np.asarray([[r[0]] for r in runs]),
+        **{k: np.asarray([[rec[i] for rec in r[1]] for r in runs])
+           for i, k in enumerate(("xy", "serving", "rate", "util", "metrics"))})
+
+    # -- heterogeneous parameters on the large layout: station tx / height / bw / freq by station
+    #    index, UE velocity / snr_tr / noise / height by UE index; 3 seeds x 2 episodes
+    layouts = json.load(open(LAYOUTS))
+    lay = layouts["large"]
+    B, U = len(lay["bs"]), lay["num_ues"]
+    bs_classes = [{"bw": 9e6, "freq": 2500, "tx": 40, "height": 50},
+                  {"bw": 9e6, "freq": 2500, "tx": 30, "height": 50},
+                  {"bw": 5e6, "freq": 1800, "tx": 35, "height": 30}]
+    ue_classes = [{"velocity": 1.5, "snr_tr": 2e-8, "noise": 1e-9, "height": 1.6},
+                  {"velocity": 10, "snr_tr": 2e-8, "noise": 1e-9, "height": 1.8},
+                  {"velocity": 3, "snr_tr": 1e-7, "noise": 2e-9, "height": 1.5}]
+    bs_cls = [i % 3 for i in range(B)]
+    ue_cls = [(i * 7) % 3 for i in range(U)]
+    runs = []
+    hseeds = [2024, 5, 77]
+    for sd in hseeds:
+        env, users = _build_mixed(ref_base, BaseStation, UserEquipment, lay["bs"],
+                                  [bs_classes[c] for c in bs_cls],
+                                  [ue_classes[c] for c in ue_cls], sd)
+        runs.append(run_episodes(env, users, episodes=2, steps=20))
+    out["large_mixed"] = dict(
+        bs_xy=np.asarray(lay["bs"], dtype=np.int64), seeds=np.asarray(hseeds),
+        velocity=np.float64(np.nan),
+        bs_class=np.asarray(bs_cls), ue_class=np.asarray(ue_cls),
+        bs_classes=json.dumps(bs_classes), ue_classes=json.dumps(ue_classes),
+        **{k: np.stack([r[k] for r in runs]) for k in runs[0]})
+    return out
+
+
+def main_extra():
+    ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
+    scratch = tempfile.mkdtemp(prefix="mev_golden_")
+    os.chdir(scratch)
+    for name, arrs in extra_fixtures(ref_base, BaseStation, UserEquipment).items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+        print("wrote", name)
+
+
 def main():
     ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
     scratch = tempfile.mkdtemp(prefix="mev_golden_")
@@ -292,4 +370,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    # --extra: only the round-2 fixtures (per-env 128 x 1024, heterogeneous parameters)
+    main_extra() if "--extra" in sys.argv[1:] else main()

@@ -13,7 +13,7 @@ DEFAULT_UE = {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
 
 # fixture name -> (num_ues, per-env ragged layout?)
 FIXTURES = ("small", "medium", "large", "small_v10", "large_v10", "mcom_custom",
-            "custom128x1024")
+            "custom128x1024", "custom128x1024_perenv")
 
 
 def load(name):

@@ -64,24 +64,31 @@ def test_bare_core_first_step_is_noop():
 
 
 @pytest.mark.parametrize("env_id", ["mobile-small-central-v0", "mobile-medium-ma-v0",
-                                    "mobile-large-central-v0"])
+                                    "mobile-large-central-v0", "mobile-large-ma-v0",
+                                    "mobile-custom-128x1024-v0"])
 def test_make_reset_step_matches_oracle(env_id):
     import mobile_env
     from oracle.vec import OracleBatch, OracleParams
     from mobile_env.scenarios.registry import LAYOUTS, spec
-    E = 64
+    sp = spec(env_id)
+    E = 64 if sp["num_ues"] <= 64 else 3
     env = mobile_env.make(env_id, num_envs=E, seed=300)
     obs, info = env.reset()
-    sp = spec(env_id)
-    lay = LAYOUTS[sp["layout"]]
-    ob = OracleBatch(OracleParams(), lay["bs"], lay["num_ues"], np.arange(E) + 300)
+    if sp["per_env_layout"]:
+        bs = env.engine.bs_xy.cpu().numpy()
+        U = sp["num_ues"]
+        ob = OracleBatch(OracleParams(velocity=float(sp["velocity"])), bs, U,
+                         np.arange(E) + 300)
+    else:
+        lay = LAYOUTS[sp["layout"]]
+        U = lay["num_ues"]
+        ob = OracleBatch(OracleParams(), lay["bs"], U, np.arange(E) + 300)
     ob.reset()
     np.testing.assert_array_equal(env.engine.ue_xy.cpu().numpy(),
                                   np.stack([ob.x, ob.y], -1))
-    for s in range(45):
+    for s in range(45 if U <= 64 else 22):
         obs, rew, term, trunc, info = env.step()
         o = ob.step()
-        U = lay["num_ues"]
         o4 = obs.cpu().numpy().reshape(E, U, 4)
         np.testing.assert_array_equal(info["serving"].cpu().numpy(), o["serving"])
         np.testing.assert_allclose(o4[..., 0], o["xy"][..., 0] / 200.0, rtol=1e-6)
@@ -115,3 +122,25 @@ def test_device_seeding_equals_host_seeding():
     np.testing.assert_array_equal(rows.cpu().numpy().view(np.uint64), want)
     st = np.random.PCG64(int(seeds[100])).state["state"]
     assert int(want[100, 0]) | (int(want[100, 1]) << 64) == st["state"]
+
+
+def test_make_custom_layouts_are_the_fixture_layouts():
+    """make("mobile-custom-128x1024-v0") draws each env's 128 stations from its seed; the
+    per-env 128 x 1024 fixture (generated by the reference on those layouts) then matches the
+    batched surface step by step: positions and serving bit-exact, rates within 1e-5."""
+    import mobile_env
+    d = load("custom128x1024_perenv")
+    E = len(d["seeds"])
+    env = mobile_env.make("mobile-custom-128x1024-v0", num_envs=E, seed=int(d["seeds"][0]))
+    np.testing.assert_array_equal(env.engine.bs_xy.cpu().numpy(), d["bs_xy"])
+    env.reset()
+    np.testing.assert_array_equal(env.engine.ue_xy.cpu().numpy(), d["init_xy"][:, 0])
+    for s in range(d["xy"].shape[1]):
+        obs, rew, term, trunc, info = env.step()
+        np.testing.assert_array_equal(env.engine.ue_xy.cpu().numpy(), d["xy"][:, s])
+        np.testing.assert_array_equal(info["serving"].cpu().numpy(), d["serving"][:, s])
+        o4 = obs.cpu().numpy().reshape(E, 1024, 4)
+        np.testing.assert_allclose(o4[..., 2], d["rate"][:, s].astype(np.float32), rtol=1e-5)
+        np.testing.assert_allclose(rew.cpu().numpy(), d["metrics"][:, s, 2], rtol=1e-5,
+                                   atol=1e-7)
+    env.close()

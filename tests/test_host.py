@@ -87,6 +87,11 @@ def test_create_rejects_bad_params_without_gpu():
         cp = EngineParams(**kw).to_c(False)
         ctx = C.c_void_p()
         assert lib.mev_create(C.byref(cp), C.byref(ctx)) == N.MEV_EINVAL
+    # a caller's channel table longer than any squared distance on a 1024 x 1024 map
+    cp = EngineParams(num_envs=4, num_ues=5, num_bs=3).to_c(False)
+    cp.rate_table_len = 2 * 1023 * 1023 + 2
+    cp.rate_table = C.c_void_p(8)  # not read: rejected first
+    assert lib.mev_create(C.byref(cp), C.byref(C.c_void_p())) == N.MEV_EINVAL
 
 
 def test_registry():
@@ -138,11 +143,17 @@ def test_lowering_builtin_plugins_and_rejects_others():
         lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
                        first_step_active=True, **{**plug, "scheduler": RateFair()})
 
-    class MyHata(OkumuraHata):
-        pass
+    class MyHata(OkumuraHata):  # overrides nothing the kernel implements: lowers
+        label = "mine"
+    lowering.check_plugins(plug["arrival"], MyHata(), plug["scheduler"], plug["movement"],
+                           plug["utility"])
+
+    class LossyHata(OkumuraHata):  # its own path loss: no kernel
+        def power_loss(self, bs, ue):
+            return 1.0
     with pytest.raises(NotImplementedError):
-        lowering.check_plugins(plug["arrival"], MyHata(), plug["scheduler"], plug["movement"],
-                               plug["utility"])
+        lowering.check_plugins(plug["arrival"], LossyHata(), plug["scheduler"],
+                               plug["movement"], plug["utility"])
     us[2].velocity = 3.0
     with pytest.raises(NotImplementedError):
         lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
@@ -232,3 +243,22 @@ def test_sums_of_two_squares_rank_index():
         d2 = int(dx * dx + dy * dy)
         if d2 <= d2max:
             assert d2 in s
+
+
+def test_store_hazard_check_on_generated_assembly():
+    """Deterministic guard for the gfx950 wide-buffer-store hazard (mev_step.hip
+    flush_pending): no buffer_store_dwordx3/x4 in the generated device assembly takes an SGPR
+    soffset (LLVM places no wait state for those), checked on `make asm` output; the checker
+    itself flags a register soffset."""
+    import shutil
+    import sys
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        pytest.skip("hipcc not available")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_store_hazard as ch
+    bad_line = "\tbuffer_store_dwordx4 v[0:3], v8, s[96:99], s4 offen"
+    assert ch.violations("_Zk:\n" + bad_line) and not ch.violations(
+        "_Zk:\n\tbuffer_store_dwordx4 v[0:3], v8, s[96:99], 0 offen")
+    text = open(ch.build_asm()).read()
+    assert ch.wide_store_count(text) > 0
+    assert ch.violations(text) == []

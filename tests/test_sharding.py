@@ -73,3 +73,67 @@ def test_shard_ranges_partition():
     cover = np.concatenate([shard_seeds(7, E, r) for r in range(world)])
     np.testing.assert_array_equal(cover, 7 + np.arange(world * E))
     assert shard_envs(E, 3) == (3 * E, 4 * E)
+
+
+def _bench_worker(rank, world, port, out_path):
+    """bench.py's N > 1 glue on CPU (gloo): per-rank seeds, the timed region with the chunk
+    plan, the final (reward, done) all-gather and the MAX-over-ranks time. The engine is a
+    stand-in that writes its rank's (reward, done) rows and takes rank-dependent time."""
+    import importlib.util
+    import sys
+    import time as _t
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mobile-env-gan_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from mobile_env.sharding import gather_final, shard_seeds
+    E, K, chunk = 5, 23, 10
+    seeds = shard_seeds(1000, E, rank)
+    plan = bench.chunk_plan(K, chunk)
+    reward = torch.zeros(E)
+    done = torch.zeros(E, dtype=torch.uint8)
+    issued = []
+
+    def issue(n):
+        issued.append(n)
+        _t.sleep(0.01 * (rank + 1) * n / chunk)
+        reward.copy_(torch.as_tensor(seeds, dtype=torch.float32) + sum(issued))
+        done.fill_(int(sum(issued) % 20 == 0))
+
+    class Ev:
+        def record(self):
+            pass
+
+    got = {}
+
+    def collective():
+        got["g"] = gather_final(reward, done)
+
+    elapsed, events = bench.timed_run(issue, plan, lambda: None, dist.barrier, Ev, collective)
+    mine = elapsed
+    elapsed = bench.max_over_ranks(elapsed)
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    if rank == 0:
+        torch.save({"plan": plan, "issued": issued, "elapsed": elapsed, "every": every,
+                    "g": got["g"], "value": world * E * K / elapsed}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_multi_rank_glue(tmp_path):
+    world = 2
+    out = str(tmp_path / "bench.pt")
+    mp.spawn(_bench_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    r = torch.load(out, weights_only=False)
+    assert r["plan"] == [10, 10, 3] and r["issued"] == r["plan"]  # exactly K = 23 steps
+    assert r["elapsed"] == max(r["every"]) and r["every"][1] > r["every"][0]
+    g = r["g"]  # [world, 2, E]: rank r's rows are its own envs (seeds 1000 + r*E + i) + 23
+    want = (1000 + np.arange(world * 5)).reshape(world, 5) + 23
+    np.testing.assert_array_equal(g[:, 0].numpy(), want.astype(np.float32))
+    np.testing.assert_array_equal(g[:, 1].numpy(), np.zeros((world, 5), np.float32))
+    assert r["value"] == world * 5 * 23 / r["elapsed"]

@@ -5,7 +5,8 @@ usage: python tools/pmc_summary.py gpurun_out/prof_TAG TAG "<bench args of the p
 
 Reads the rocprofv3 CSVs of the passes (kt: kernel trace + stats; fetch / write / sq / sq2: PMC
 counters) and keeps the dispatches of the launch the bench times:
-  * --launch fused (default): the fused multi-step kernel k_steps_packed (20 steps each);
+  * --launch fused (default): the fused multi-step kernel k_steps_packed (--chunk steps each,
+    one dispatch per chunk);
   * --launch single / split: the one-step kernels k_step_packed / k_step_block.
 Writes
   profiles/<tag>_kernel_stats.csv   -- rocprofv3 --stats summary (copied)
@@ -56,7 +57,7 @@ def main():
         elif t == "--chunk":
             chunk = int(toks[i + 1])
     kre = FUSED_RE if launch == "fused" else SINGLE_RE
-    steps = -(-steps // chunk) * chunk  # bench.py rounds up to whole chunks
+    chunk = min(chunk, steps) if steps else chunk  # bench.py: exactly `steps`, chunk <= steps
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
 
@@ -77,7 +78,7 @@ def main():
                    if kre.search(r.get("Kernel_Name", "")))
     steps_per_launch = chunk if launch == "fused" else 1
     parts = 2 if launch == "split" else 1
-    n_timed = steps // steps_per_launch * parts
+    n_timed = -(-steps // steps_per_launch) * parts  # whole chunks + the remainder launch
     if trace and n_timed:
         timed = trace[-n_timed:]
         span = max(e for _, e in timed) - timed[0][0]
