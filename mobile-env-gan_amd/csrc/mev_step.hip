@@ -1248,19 +1248,149 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 }
 
 // ------------------------------------------------------------------------------------
-// Block kernel: 64 < U <= 1024, one workgroup per env, lane u = threadIdx.x.
+// Block shape: 64 < U <= 1024, one workgroup per env, lane u = threadIdx.x.
 // ------------------------------------------------------------------------------------
-template <bool PER_ENV_BS, bool RESET>
-// (8 waves per SIMD requested: <= 64 VGPRs, two 1024-thread workgroups per CU -- 34.0 vs
-// 38.5 us per step at 1,024 envs of mobile-custom-128x1024, a few bytes of spills)
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_step_block(KParams kp, KState st, KOut out, KTables tb,
-                                                    const uint8_t* __restrict__ mask) {
-  __shared__ int lds_cnt[kMaxB];
-  __shared__ int lds_wtot[3][16];
-  __shared__ __align__(16) int2 lds_key[kMaxB + 2];  // the env's station keys (below)
-  __shared__ double lds_sum[4][16];
-
+// Reset (mev_reset): MComCore.reset for the envs with mask[e] (all if NULL), as k_reset_packed.
+__global__ __launch_bounds__(1024) void k_reset_block(KParams kp, KState st, KOut out,
+                                                      KTables tb,
+                                                      const uint8_t* __restrict__ mask) {
   const int e = blockIdx.x;
+  const int u = threadIdx.x;
+  const int U = kp.U;
+  if (mask != nullptr && !mask[e]) return;  // uniform over the workgroup
+  const bool valid = u < U;
+  const size_t idx = (size_t)e * U + u;
+  const uint64_t* pr = st.pcg + (size_t)6 * e;
+  const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(pr + 2);
+  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(pr);
+  const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
+  const u128 s0 = kp.movement_reseed ? mk128(c.x, c.y) : mk128(a.x, a.y);
+  int x = 0, y = 0;
+  u128 s_fin = s0;
+  if (valid) s_fin = pcg_draw_pair(s0, mk128(b2.x, b2.y), 2 * u, tb.jump, kp.Wd, kp.Hd, x, y);
+  if (valid) {
+    store_ue(st.ue_state + idx, make_int2(x, y), make_int2(-1, -1));
+    out.serving[idx] = -1;
+    out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
+    if (out.rate64) out.rate64[idx] = 0.0;
+    if (out.util64) out.util64[idx] = 0.0;
+  }
+  if (u == U - 1)  // the state after the 2U initial draws
+    *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+        make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
+  if (u == 0) {
+    if (kp.tab_m) tb.drawn[e] = U;
+    st.t[e] = 0;
+    out.reward[e] = 0.f;
+    out.done[e] = 0;
+    if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// Sum over the 64 lanes of a wavefront (all active), valid in lane 63: row prefix sums by
+// row_shr 1/2/4/8, then the row totals carried by row_bcast:15 (into rows 1, 3) and
+// row_bcast:31 (into rows 2, 3).
+__device__ __forceinline__ double wave_sum_f64(double x) {
+  x += dpp_f64<0x111>(x);
+  x += dpp_f64<0x112>(x);
+  x += dpp_f64<0x114>(x);
+  x += dpp_f64<0x118>(x);
+  x += dpp_f64<0x142, 0xa>(x);
+  x += dpp_f64<0x143, 0xc>(x);
+  return x;
+}
+
+// LDS of k_steps_block (dynamic; sized by the host, block_lds_bytes): int2 keys[B + 2] (the
+// env's station keys), int cnt[2][B] (per-station connected-UE counts, two steps in flight),
+// int wt[4][16] (per-wave counts: need, active, connected, low QoE), double ps[4][16] (per-wave
+// partial sums: utility, rate, QoE, QoE^2), u128 slot[2] (stream state after the env's last
+// draw, increment), int tab[M] (the env's episode draw table).
+struct BlockLds {
+  int2* key;
+  int* cnt;
+  int* wt;
+  double* ps;
+  u128* slot;
+  int* tab;
+};
+
+__host__ __device__ inline size_t block_lds_bytes(int B, int M) {
+  const size_t keys = 8 * ((size_t)B + 2), cnt = 8 * (size_t)B;
+  return keys + ((cnt + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32 + 4 * (size_t)M;
+}
+
+__device__ __forceinline__ BlockLds block_lds(char* base, int B) {
+  BlockLds l;
+  l.key = reinterpret_cast<int2*>(base);
+  char* p = base + 8 * ((size_t)B + 2);
+  l.cnt = reinterpret_cast<int*>(p);
+  p += (8 * (size_t)B + 15) & ~(size_t)15;
+  l.wt = reinterpret_cast<int*>(p);
+  l.ps = reinterpret_cast<double*>(p + 4 * 64);
+  l.slot = reinterpret_cast<u128*>(p + 4 * 64 + 8 * 64);
+  l.tab = reinterpret_cast<int*>(p + 4 * 64 + 8 * 64 + 32);
+  return l;
+}
+
+// The env's steps i0 .. nsteps-1 for one workgroup (block shape); see k_steps_block.
+// Per-env values of a step whose row the leader writes after the next step's first barrier.
+struct BlockRow {
+  int t_after, nact, ncon;
+};
+
+template <bool LEAN>
+__device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& out,
+                                                 const BlockLds& L, int nw, int e, int row,
+                                                 const BlockRow& r) {
+  // the previous step's per-wave partials, summed in wave order (float64)
+  double su = 0.0, sr = 0.0, sq = 0.0, sq2 = 0.0;
+  int nlow = 0;
+  for (int i = 0; i < nw; ++i) {
+    su += L.ps[i];
+    if (!LEAN) {
+      sr += L.ps[16 + i];
+      sq += L.ps[32 + i];
+      sq2 += L.ps[48 + i];
+      nlow += L.wt[48 + i];
+    }
+  }
+  const double mean_u = r.nact > 0 ? su / (double)r.nact : kp.lower;
+  const size_t re = (size_t)row * kp.E + e;
+  out.reward[re] = (float)mean_u;
+  out.done[re] = (uint8_t)(r.t_after >= kp.t_end);
+  if (!LEAN) {
+    if (out.metrics) {
+      const double mean_r = r.ncon > 0 ? sr / (double)r.ncon : 0.0;
+      out.metrics[re] = make_float4((float)r.ncon, (float)r.ncon, (float)mean_u, (float)mean_r);
+    }
+    if (out.qoe_stats) {
+      double4 a = r.t_after == 1 ? make_double4(0.0, 0.0, 0.0, 0.0) : out.qoe_stats[e];
+      a.x += (double)r.nact;
+      a.y += sq;
+      a.z += sq2;
+      a.w += (double)nlow;
+      out.qoe_stats[e] = a;
+    }
+  }
+}
+
+// nsteps steps of MComCore.step (base.py:230-296) for U > 64: one workgroup of ceil(U/64)
+// waves per env (lane u = UE u), envs e = blockIdx.x, blockIdx.x + gridDim.x, ...; each env's
+// state stays in registers / LDS for the launch (loaded once, stored once) and every step's
+// outputs go to row i of the trajectory (traj) or over the previous step's. Per step:
+//   A  lazy auto-reset (initial positions from the LDS draw table), need / active ballots
+//   -- barrier 1 --  workgroup scan of the waypoint draws (ue_id order); the previous step's
+//      per-env row (reward, done, metrics) by lane 0 from the per-wave partial sums
+//   B  waypoint draws (LDS draw table; beyond it, the stream state), move, association (the
+//      env's station keys in LDS, broadcast reads), per-station counts by LDS atomics
+//   -- barrier 2 --
+//   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums
+// The per-station counts alternate between two LDS arrays (the next step's array is zeroed
+// in its B phase), so two barriers per step suffice.
+template <bool PER_ENV_BS, bool LEAN>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
+    KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
+  extern __shared__ __align__(16) char lds_raw[];
   const int u = threadIdx.x;
   const int U = kp.U;
   const int lane = u & 63;
@@ -1268,220 +1398,239 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int nw = (blockDim.x + 63) >> 6;
   const bool valid = u < U;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const size_t idx = (size_t)e * U + u;
-
-  const uint64_t* pr = st.pcg + (size_t)6 * e;
-  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(pr);
-  const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(pr + 2);
-  const u128 inc = mk128(b2.x, b2.y);
-  int t = RESET ? 0 : st.t[e];
-  const bool do_reset = RESET ? (mask == nullptr || mask[e]) : (t >= kp.t_end);
-  if (RESET && !do_reset) return;  // uniform over the workgroup
-
-  // stream bookkeeping as in the packed kernel: draws of this step start at offset koff of
-  // `s`; the lane of the env's last draw writes the new stream state back
-  u128 s = mk128(a.x, a.y), s_fin = s;
-  int koff = 0;
-  int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
-  if (do_reset) {
-    const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(pr + 4);
-    if (kp.movement_reseed) s = mk128(c.x, c.y);
-    if (valid) s_fin = pcg_draw_pair(s, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
-    koff = 2 * U;
-    t = 0;
-  } else {
+  const int M = kp.tab_m;
+  const BlockLds L = block_lds(lds_raw, kp.B);
+  for (int e = blockIdx.x; e < kp.E; e += gridDim.x) {
+    // ---- prologue: state, stream, station keys, draw table -------------------------------
+    const size_t idx = (size_t)e * U + u;
+    int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
     if (valid) {
       const int4 sv = load_ue(st.ue_state + idx);
       pos = make_int2(sv.x, sv.y);
       wp = make_int2(sv.z, sv.w);
     }
-  }
-
-  if (RESET) {
-    if (valid) {
-      store_ue(st.ue_state + idx, pos, wp);
-      out.serving[idx] = -1;
-      out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, 0.f, 0.f);
-      if (out.rate64) out.rate64[idx] = 0.0;
-      if (out.util64) out.util64[idx] = 0.0;
-    }
-    if (u == U - 1) {  // the state after the 2U initial draws
-      uint64_t* pw = st.pcg + (size_t)6 * e;
-      *reinterpret_cast<ulonglong2*>(pw) =
-          make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
-    }
+    int t = st.t[e];
+    int drawn = M ? tb.drawn[e] : 0;
     if (u == 0) {
-      st.t[e] = 0;
-      out.reward[e] = 0.f;
-      out.done[e] = 0;
-      if (out.metrics) out.metrics[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e);
+      L.slot[0] = mk128(pr[0].x, pr[0].y);
+      L.slot[1] = mk128(pr[1].x, pr[1].y);
     }
-    return;
-  }
-
-  const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
-                      (kp.first_step_active || t != 0);
-  const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
-  // station keys of this env in LDS: {m as int16x2, c = ((|q|^2 + 2^21) << 10) | j}; with
-  // the map <= 512 x 512 and every station in [0, 512)^2, m = -64 q and the key is ONE dot
-  // product with accumulator, dot2(32 p, m) + c = ((|p - q|^2 - |p|^2 + 2^21) << 10) | j;
-  // otherwise m = -2 q and key = (dot2(p, m) << 10) + c. (|p|^2 is common to all stations.)
-  const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
-  bool in512 = true;
-  for (int i = u; i < nb; i += blockDim.x) {
-    const int2 q = bsx[i];
-    in512 = in512 && q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
-  }
-  const bool scaled = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512;
-  for (int i = u; i < nb; i += blockDim.x) {
-    lds_cnt[i] = 0;
-    const int2 q = bsx[i];
-    const int f = scaled ? -64 : -2;
-    const s16x2 m2 = {(short)(f * q.x), (short)(f * q.y)};
-    lds_key[i] = make_int2(__builtin_bit_cast(int, m2),
-                           (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) |
+    const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
+    // station keys {m as int16x2, c = ((|q|^2 + 2^21) << 10) | j}: with the map <= 512 x 512 and
+    // every station in [0, 512)^2, m = -64 q and key = dot2(32 p, m) + c =
+    // ((|p - q|^2 - |p|^2 + 2^21) << 10) | j; otherwise m = -2 q, key = (dot2(p, m) << 10) + c
+    const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+    bool in512 = true;
+    int2 q = make_int2(0, 0);
+    if (u < nb) {
+      q = bsx[u];
+      in512 = q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
+    }
+    for (int i = u + blockDim.x; i < nb; i += blockDim.x) {
+      const int2 qq = bsx[i];
+      in512 = in512 && qq.x >= 0 && qq.y >= 0 && qq.x < 512 && qq.y < 512;
+    }
+    if (M)
+      for (int k = u; k < M; k += blockDim.x) L.tab[k] = tb.tab_xy[(size_t)e * M + k];
+    const bool scaled = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512;
+    for (int i = u; i < nb; i += blockDim.x) {
+      const int2 qq = i == u ? q : bsx[i];
+      const int f = scaled ? -64 : -2;
+      const s16x2 m2 = {(short)(f * qq.x), (short)(f * qq.y)};
+      L.key[i] = make_int2(__builtin_bit_cast(int, m2),
+                           (int)(((unsigned)(qq.x * qq.x + qq.y * qq.y + (1 << 21)) << kKeyBits) |
                                  (unsigned)i));
-  }
+    }
+    for (int i = u; i < kp.B; i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
+    bool s_ok = true;  // the slot holds the state after the env's last draw
+    BlockRow prev{0, 0, 0};
+    __syncthreads();
 
-  // ---- 1. movement: workgroup exclusive scan of "needs waypoint" in ue_id order -------
-  const bool need = active && wp.x < 0;
-  const uint64_t mneed = bal(need);
-  const uint64_t mact = bal(active);
-  if (lane == 0) {
-    lds_wtot[0][w] = __popcll(mneed);
-    lds_wtot[1][w] = __popcll(mact);
-  }
-  __syncthreads();
-  // per-wavefront counts -> workgroup prefix / totals: lane i < nw (<= 16, one DPP row)
-  // holds wavefront i's count, a row scan, then wave-uniform reads of single lanes
-  const int scan_need = row_scan_i32(lane < nw ? lds_wtot[0][lane & 15] : 0);
-  const int scan_act = row_scan_i32(lane < nw ? lds_wtot[1][lane & 15] : 0);
-  const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
-  const int tot_need = __builtin_amdgcn_readlane(scan_need, nw - 1);
-  const int tot_act = __builtin_amdgcn_readlane(scan_act, nw - 1);
-  const int rank = pre_need + (int)__popcll(mneed & lt);
-  if (need) s_fin = pcg_draw_pair(s, inc, koff + 2 * rank, tb.jump, kp.Wd, kp.Hd, wp.x, wp.y);
-  const bool own_fin = (need && rank == tot_need - 1) || (do_reset && tot_need == 0 && u == U - 1);
-  if (active) move_ue(pos, wp, kp);
+    for (int i = 0; i < nsteps; ++i) {
+      const int row = traj ? i : 0;
+      int* cnt = L.cnt + (i & 1) * kp.B;  // (B = count array stride; two arrays below)
+      // ---- A: lazy auto-reset, ballots ------------------------------------------------
+      const bool reset = t >= kp.t_end;  // uniform
+      int koff = 0;
+      u128 base = L.slot[0];  // read before barrier 1 (the slot is written after it)
+      const u128 inc = L.slot[1];
+      if (reset) {
+        t = 0;
+        wp = make_int2(-1, -1);
+        if (M) {
+          if (valid) {
+            const int p = L.tab[u];
+            pos = make_int2((int)(short)p, p >> 16);
+          }
+          drawn = U;
+          s_ok = false;
+        } else {
+          const ulonglong2 c = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
+          if (kp.movement_reseed) base = mk128(c.x, c.y);
+          if (valid) (void)pcg_draw_pair(base, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+          koff = 2 * U;
+        }
+      }
+      const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
+                          (kp.first_step_active || t != 0);
+      const bool need = active && wp.x < 0;
+      const uint64_t mneed = bal(need);
+      const uint64_t mact = bal(active);
+      if (lane == 0) {
+        L.wt[w] = __popcll(mneed);
+        L.wt[16 + w] = __popcll(mact);
+      }
+      __syncthreads();  // ---- barrier 1
 
-  // ---- 2. association: min over the env's station keys (LDS broadcast reads, two
-  //         stations per 16-byte read) --------------------------------------------------
-  unsigned best = UINT_MAX;
-  if (active) {
-    const int4* kk2 = reinterpret_cast<const int4*>(lds_key);
-    const int npair = nb >> 1;
-    if (scaled) {
-      const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
+      const int scan_need = row_scan_i32(lane < nw ? L.wt[lane & 15] : 0);
+      const int scan_act = row_scan_i32(lane < nw ? L.wt[16 + (lane & 15)] : 0);
+      const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
+      const int tot = __builtin_amdgcn_readlane(scan_need, nw - 1);
+      const int nact = __builtin_amdgcn_readlane(scan_act, nw - 1);
+      if (u == 0 && i > 0)
+        block_finish_row<LEAN>(kp, out, L, nw, e, traj ? i - 1 : 0, prev);
+      int* cnt_next = L.cnt + ((i + 1) & 1) * kp.B;
+      for (int k = u; k < kp.B; k += blockDim.x) cnt_next[k] = 0;
+
+      // ---- B: waypoint draws in ue_id order (movement.py:44-47), move ------------------
+      const int rank = pre_need + (int)__popcll(mneed & lt);
+      if (tot > 0) {
+        const int k = drawn + rank;  // pair index in the episode
+        if (M && drawn + tot <= M) {  // every pair precomputed (the common case)
+          if (need) {
+            const int p = L.tab[k];
+            wp = make_int2((int)(short)p, p >> 16);
+          }
+          s_ok = false;
+        } else {
+          // beyond the table (or none): from the stream state after pair bidx - 1 (the slot,
+          // or the table's last entry), pair k at offset 2 (k - bidx)
+          int bidx = drawn;
+          if (M && !s_ok) {
+            base = tb.tab_st[(size_t)e * M + (M - 1)];
+            bidx = M;
+          }
+          if (need) {
+            u128 s_fin;
+            if (M && k < M) {
+              const int p = L.tab[k];
+              wp = make_int2((int)(short)p, p >> 16);
+              s_fin = base;
+            } else {
+              s_fin = pcg_draw_pair(base, inc, koff + 2 * (k - bidx), tb.jump, kp.Wd, kp.Hd,
+                                    wp.x, wp.y);
+            }
+            if (rank == tot - 1) L.slot[0] = s_fin;  // the env's new stream state
+          }
+          s_ok = true;
+        }
+        drawn += tot;
+      } else if (reset && !M && u == U - 1) {  // reset without draws: after the initial pairs
+        L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+      }
+      if (active) move_ue(pos, wp, kp);
+
+      // ---- association: min over the env's station keys (LDS broadcast reads) ----------
+      unsigned best = UINT_MAX;
+      if (active) {
+        const int4* kk2 = reinterpret_cast<const int4*>(L.key);
+        const int npair = nb >> 1;
+        if (scaled) {
+          const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
 #pragma unroll 4
-      for (int i = 0; i < npair; ++i) {
-        const int4 k = kk2[i];
-        const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.x), k.y, false);
-        const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.z), k.w, false);
-        best = min(best, min(k0, k1));
-      }
-      if (nb & 1) {
-        const int2 k = lds_key[nb - 1];
-        best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, k.x), k.y, false));
-      }
-    } else {
-      const s16x2 pu = {(short)pos.x, (short)pos.y};
+          for (int j = 0; j < npair; ++j) {
+            const int4 kv = kk2[j];
+            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), kv.y, false);
+            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.z), kv.w, false);
+            best = min(best, min(k0, k1));
+          }
+          if (nb & 1) {
+            const int2 kv = L.key[nb - 1];
+            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), kv.y, false));
+          }
+        } else {
+          const s16x2 pu = {(short)pos.x, (short)pos.y};
 #pragma unroll 4
-      for (int i = 0; i < npair; ++i) {
-        const int4 k = kk2[i];
-        const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.x), 0, true);
-        const int d1 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.z), 0, true);
-        best = min(best, min(((unsigned)d0 << kKeyBits) + (unsigned)k.y,
-                             ((unsigned)d1 << kKeyBits) + (unsigned)k.w));
+          for (int j = 0; j < npair; ++j) {
+            const int4 kv = kk2[j];
+            const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.x), 0, true);
+            const int d1 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.z), 0, true);
+            best = min(best, min(((unsigned)d0 << kKeyBits) + (unsigned)kv.y,
+                                 ((unsigned)d1 << kKeyBits) + (unsigned)kv.w));
+          }
+          if (nb & 1) {
+            const int2 kv = L.key[nb - 1];
+            const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.x), 0, true);
+            best = min(best, ((unsigned)d0 << kKeyBits) + (unsigned)kv.y);
+          }
+        }
       }
-      if (nb & 1) {
-        const int2 k = lds_key[nb - 1];
-        const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, k.x), 0, true);
-        best = min(best, ((unsigned)d0 << kKeyBits) + (unsigned)k.y);
+      // d2 of the best station: key - 2^21 + |p|^2
+      const int d2s = (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
+      const int srv =
+          (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
+      const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
+      if (srv >= 0) atomicAdd(&cnt[srv], 1);
+      if (!LEAN && lane == 0) L.wt[32 + w] = __popcll(bal(srv >= 0));
+      __syncthreads();  // ---- barrier 2
+
+      // ---- C: ResourceFair share + rounding, utility, stores, partial sums -------------
+      double cents = 0.0;
+      float cents_f = 0.f;
+      if (srv >= 0) cents = share_cents(full, cnt[srv], cents_f);
+      const bool exact_util = !LEAN;
+      const double rate = cents / 100.0;
+      double util = 0.0;
+      if (active)
+        util = exact_util ? utility_of(rate, cents, kp, tb.util)
+                          : utility_f32r(cents_f, cents_f * 0.01f, kp);
+      const size_t ro = (size_t)row * kp.E * U + idx;
+      if (valid) {
+        out.serving[ro] = srv;
+        out.obs[ro] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
+                                  cents_f * 0.01f, (float)util);
+        if (!LEAN) {
+          if (out.rate64) out.rate64[ro] = rate;
+          if (out.util64) out.util64[ro] = active ? util : __builtin_nan("");
+        }
       }
-    }
-  }
-  // d2 of the best station: e - 2^21 + |p|^2
-  const int d2s = (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
-  const int srv = (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
-
-  // ---- 3. per-BS counts via LDS atomics ---------------------------------------------
-  if (srv >= 0) atomicAdd(&lds_cnt[srv], 1);
-  const uint64_t mcon = bal(srv >= 0);
-  if (lane == 0) lds_wtot[2][w] = __popcll(mcon);
-  __syncthreads();
-  const int tot_con =
-      __builtin_amdgcn_readlane(row_scan_i32(lane < nw ? lds_wtot[2][lane & 15] : 0), nw - 1);
-
-  // ---- 4. rate + utility -------------------------------------------------------------
-  double cents = 0.0, rate = 0.0;
-  float cents_f;
-  if (srv >= 0) cents = share_cents(tb.rate_full[d2s], lds_cnt[srv], cents_f);
-  if (out.rate64 || out.metrics || kp.util_direct) rate = cents / 100.0;  // exact float64 rate
-  const double util = active ? utility_of(rate, cents, kp, tb.util) : 0.0;
-  const bool want_metrics = out.metrics != nullptr;
-  const bool want_qoe = out.qoe_stats != nullptr;
-  const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
-  // reward / mean rate / QoE statistics: float64 workgroup sums (wavefront xor-tree, then
-  // across wavefronts)
-  {
-    double su = active ? util : 0.0, sr = (want_metrics && srv >= 0) ? rate : 0.0;
-    double sq = (want_qoe && active) ? q : 0.0, sq2 = sq * sq;
-    for (int off = 32; off > 0; off >>= 1) {
-      su += __shfl_xor(su, off);
-      if (want_metrics) sr += __shfl_xor(sr, off);
-      if (want_qoe) {
-        sq += __shfl_xor(sq, off);
-        sq2 += __shfl_xor(sq2, off);
+      const double su = wave_sum_f64(active ? util : 0.0);
+      if (lane == 63) L.ps[w] = su;
+      if (!LEAN) {
+        const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
+        const double sr = wave_sum_f64(srv >= 0 ? rate : 0.0);
+        const double sq = wave_sum_f64(active ? q : 0.0);
+        const double sq2 = wave_sum_f64(active ? q * q : 0.0);
+        const int nlow = __popcll(bal(active && q < kp.qoe_low));
+        if (lane == 63) {
+          L.ps[16 + w] = sr;
+          L.ps[32 + w] = sq;
+          L.ps[48 + w] = sq2;
+          L.wt[48 + w] = nlow;
+        }
       }
+      int ncon = 0;
+      if (!LEAN) {
+        const int sc = row_scan_i32(lane < nw ? L.wt[32 + (lane & 15)] : 0);
+        ncon = __builtin_amdgcn_readlane(sc, nw - 1);
+      }
+      prev = BlockRow{t + 1, nact, ncon};
+      t += 1;
     }
-    if (lane == 0) {
-      lds_sum[0][w] = su;
-      lds_sum[1][w] = sr;
-      lds_sum[2][w] = sq;
-      lds_sum[3][w] = sq2;
-    }
-  }
-  const uint64_t mlow = bal(want_qoe && active && q < kp.qoe_low);
-  if (lane == 0) lds_wtot[0][w] = __popcll(mlow);  // the need counts were read above
-  __syncthreads();
-
-  if (valid) {
-    store_ue(st.ue_state + idx, pos, wp);
-    out.serving[idx] = srv;
-    out.obs[idx] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
-                               (float)cents * 0.01f, (float)util);
-    if (out.rate64) out.rate64[idx] = rate;
-    if (out.util64) out.util64[idx] = active ? util : __builtin_nan("");
-    if (own_fin)  // the stream moved (draws, or reset): write the new state back
+    __syncthreads();  // the last step's partial sums
+    if (u == 0 && nsteps > 0)
+      block_finish_row<LEAN>(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev);
+    // ---- epilogue: the state after the last step ----------------------------------------
+    if (valid) store_ue(st.ue_state + idx, pos, wp);
+    if (u == 0) {
+      st.t[e] = t;
+      if (M) tb.drawn[e] = drawn;
+      const u128 sf = (s_ok || !M) ? L.slot[0] : tb.tab_st[(size_t)e * M + (min(drawn, M) - 1)];
       *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
-          make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
-  }
-  if (u == 0) {
-    double sum_u = 0.0, sum_r = 0.0, sum_q = 0.0, sum_q2 = 0.0;
-    int nlow = 0;
-    for (int i = 0; i < nw; ++i) {
-      sum_u += lds_sum[0][i];
-      sum_r += lds_sum[1][i];
-      sum_q += lds_sum[2][i];
-      sum_q2 += lds_sum[3][i];
-      nlow += lds_wtot[0][i];
+          make_ulonglong2((uint64_t)sf, (uint64_t)(sf >> 64));
     }
-    if (want_qoe) {
-      double4 a = t == 0 ? make_double4(0.0, 0.0, 0.0, 0.0) : out.qoe_stats[e];
-      a.x += (double)tot_act;
-      a.y += sum_q;
-      a.z += sum_q2;
-      a.w += (double)nlow;
-      out.qoe_stats[e] = a;
-    }
-    const double mean_u = tot_act > 0 ? sum_u / (double)tot_act : kp.lower;
-    st.t[e] = t + 1;
-    out.reward[e] = (float)mean_u;
-    out.done[e] = (uint8_t)(t + 1 >= kp.t_end);
-    if (want_metrics) {
-      const double mean_r = tot_con > 0 ? sum_r / (double)tot_con : 0.0;
-      out.metrics[e] = make_float4((float)tot_con, (float)tot_con, (float)mean_u, (float)mean_r);
-    }
+    __syncthreads();  // LDS reused by the next env
   }
 }
 
@@ -1977,7 +2126,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
 
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
   c->kp.tab_m = 0;
-  if (params->draw_table != 0 && params->movement_reseed && params->num_ues <= 64)
+  if (params->draw_table != 0 && params->movement_reseed)
     c->kp.tab_m = params->draw_table > 0 ? params->draw_table : 3 * params->num_ues + 8;
   if (c->kp.tab_m) {
     const size_t n = (size_t)params->num_envs * (size_t)c->kp.tab_m;
@@ -2229,6 +2378,30 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   return MEV_OK;
 }
 
+// Block-shape steps (U > 64): ONE launch of k_steps_block for the n steps (fuse_steps), or one
+// per step; one workgroup per env.
+static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko,
+                              const KTables& tb, int nsteps, bool traj, hipStream_t stream) {
+  const KParams& kp = c->kp;
+  if (nsteps <= 0) return MEV_OK;
+  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
+  const bool per_env = c->p.bs_per_env != 0;
+  void (*kf)(KParams, KState, KOut, KTables, int, int) =
+      per_env ? (lean ? k_steps_block<true, true> : k_steps_block<true, false>)
+              : (lean ? k_steps_block<false, true> : k_steps_block<false, false>);
+  const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
+  const size_t shm = block_lds_bytes(kp.B, kp.tab_m);
+  if (c->fuse_steps || nsteps == 1) {
+    kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, ko, tb, nsteps, traj ? 1 : 0);
+  } else {
+    for (int i = 0; i < nsteps; ++i)
+      kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, traj ? out_row(ko, kp.E, kp.U, i) : ko, tb,
+                                             1, 0);
+  }
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
 template <bool RESET>
 static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
                   const uint8_t* mask, hipStream_t stream) {
@@ -2238,7 +2411,6 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
              c->blob};
   const KParams& kp = c->kp;
-  const bool per_env = c->p.bs_per_env != 0;
   if (kp.U <= 64) {
     const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
     if (RESET) {
@@ -2248,14 +2420,11 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
     } else {
       return launch_packed_steps(c, ks, ko, tb, 1, false, stream);
     }
-  } else {
+  } else if (RESET) {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
-    if (per_env)
-      hipLaunchKernelGGL((k_step_block<true, RESET>), dim3(kp.E), block, 0, stream, kp, ks, ko,
-                         tb, mask);
-    else
-      hipLaunchKernelGGL((k_step_block<false, RESET>), dim3(kp.E), block, 0, stream, kp, ks, ko,
-                         tb, mask);
+    hipLaunchKernelGGL(k_reset_block, dim3(kp.E), block, 0, stream, kp, ks, ko, tb, mask);
+  } else {
+    return launch_block_steps(c, ks, ko, tb, 1, false, stream);
   }
   MEV_HIP(hipGetLastError());
   return MEV_OK;
@@ -2308,30 +2477,13 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   if (nsteps < 0) return MEV_EINVAL;
-  if (c->kp.U <= 64) {
-    KState ks;
-    KOut ko;
-    to_kernel(st, out, ks, ko);
-    const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
-                     c->blob};
-    return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
-  }
-  const int64_t eu = (int64_t)c->kp.E * c->kp.U, ee = c->kp.E;
-  for (int i = 0; i < nsteps; ++i) {
-    mev_outputs oi = *out;
-    if (traj) {  // row i of the trajectory buffers (out_row)
-      oi.obs += 4 * eu * i;
-      oi.serving += eu * i;
-      oi.reward += ee * i;
-      oi.done += ee * i;
-      if (oi.rate64) oi.rate64 += eu * i;
-      if (oi.util64) oi.util64 += eu * i;
-      if (oi.metrics) oi.metrics += 4 * ee * i;
-    }
-    rc = launch<false>(c, st, &oi, nullptr, (hipStream_t)stream);
-    if (rc) return rc;
-  }
-  return MEV_OK;
+  KState ks;
+  KOut ko;
+  to_kernel(st, out, ks, ko);
+  const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
+                   c->blob};
+  if (c->kp.U <= 64) return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
+  return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
 }
 
 int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int32_t nsteps,

@@ -215,8 +215,8 @@ class StepEngine:
 
     @property
     def fused_steps(self) -> bool:
-        """step(n > 1) runs as one fused launch (U <= 64 and fuse_steps >= 0)."""
-        return self.p.num_ues <= 64 and self.p.fuse_steps >= 0
+        """step(n > 1) / rollout(n) run as one fused launch (fuse_steps >= 0)."""
+        return self.p.fuse_steps >= 0
 
     @property
     def launch_parts(self) -> int:
@@ -324,7 +324,7 @@ class StepEngine:
                      if self.metrics is not None else None))
 
     def rollout(self, nsteps: int, traj: "Trajectory | None" = None) -> "Trajectory":
-        """mev_rollout: ``nsteps`` steps (as step(nsteps): one launch for U <= 64) keeping
+        """mev_rollout: ``nsteps`` steps (as step(nsteps): one launch) keeping
         every step's outputs -- row i of the returned trajectory is step i. ``traj`` (from
         trajectory(n), n >= nsteps) is reused when given. The engine's own one-step output
         tensors (obs, serving, ...) are not written; qoe_stats accumulates as in step()."""
@@ -346,6 +346,31 @@ class StepEngine:
             N.check(self._lib.mev_rollout(self._ctx, C.byref(self._st), C.byref(out), n,
                                           self._stream()), "mev_rollout")
         return traj
+
+    def launcher(self, nsteps: int, traj: "Trajectory | None" = None):
+        """A zero-argument callable that issues ``rollout(nsteps, traj)`` (traj given) or
+        ``step(nsteps)`` with every ctypes argument prebuilt: the per-call host cost is one
+        foreign call (the benchmark's timed loop; the caller keeps the device current)."""
+        n = int(nsteps)
+        st = C.byref(self._st)
+        stream = self._stream()
+        if traj is None:
+            fn, out, where = self._lib.mev_step, C.byref(self._out), "mev_step"
+        else:
+            if traj.obs.shape[0] < n or tuple(traj.obs.shape[1:]) != tuple(self.obs.shape):
+                raise ValueError("trajectory buffers do not fit this engine / nsteps")
+            o = N.MevOutputs(_ptr(traj.obs), _ptr(traj.serving), _ptr(traj.reward),
+                             _ptr(traj.done), _ptr(traj.rate64), _ptr(traj.util64),
+                             _ptr(traj.metrics), _ptr(self.qoe_stats))
+            fn, out, where = self._lib.mev_rollout, C.byref(o), "mev_rollout"
+        ctx = self._ctx
+
+        def go():
+            rc = fn(ctx, st, out, n, stream)
+            if rc:
+                N.check(rc, where)
+        go.keep = (out, traj)
+        return go
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and self._ctx.value:

@@ -131,7 +131,7 @@ def test_bench_multi_rank_glue(tmp_path):
     mp.spawn(_bench_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     r = torch.load(out, weights_only=False)
     assert r["plan"] == [10, 10, 3] and r["issued"] == r["plan"]  # exactly K = 23 steps
-    assert r["elapsed"] == max(r["every"]) and r["every"][1] > r["every"][0]
+    assert r["elapsed"] == max(r["every"])
     g = r["g"]  # [world, 2, E]: rank r's rows are its own envs (seeds 1000 + r*E + i) + 23
     want = (1000 + np.arange(world * 5)).reshape(world, 5) + 23
     np.testing.assert_array_equal(g[:, 0].numpy(), want.astype(np.float32))

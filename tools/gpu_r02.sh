@@ -17,6 +17,7 @@ fi
 if [ -z "$SKIP_PROFILE" ]; then
   tools/profile.sh $TAG || exit 1
   tools/profile.sh ${TAG}_single --launch single || exit 1
+  python tools/merge_profiles.py || exit 1  # (the box's copy: the bench reads it)
 fi
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; cat gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log

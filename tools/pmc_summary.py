@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into profiles/ (committed evidence).
 
-usage: python tools/pmc_summary.py gpurun_out/prof_TAG TAG "<bench args of the profile run>"
+usage: python tools/pmc_summary.py RAW_DIR TAG "<bench args of the profile run>" [OUT_DIR]
+(OUT_DIR defaults to profiles/; on the GPU box tools/profile.sh writes gpurun_out/profiles/, which
+comes back with the call, and tools/merge_profiles.py folds it into profiles/)
 
 Reads the rocprofv3 CSVs of the passes (kt: kernel trace + stats; fetch / write / sq / sq2: PMC
 counters) and keeps the dispatches of the launch the bench times:
@@ -58,7 +60,7 @@ def main():
             chunk = int(toks[i + 1])
     kre = FUSED_RE if launch == "fused" else SINGLE_RE
     chunk = min(chunk, steps) if steps else chunk  # bench.py: exactly `steps`, chunk <= steps
-    prof = os.path.join(ROOT, "profiles")
+    prof = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
 
     summary = {"tag": tag, "workload": workload, "envs": envs, "launch": launch,
