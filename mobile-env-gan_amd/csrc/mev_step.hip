@@ -1314,15 +1314,18 @@ struct BlockLds {
   int* tab;
 };
 
+// (the keys live in a static array: its 16-byte alignment is known to the compiler, which
+// then reads two stations per broadcast ds_read_b128 -- from the dynamic area it issued four
+// ds_read2_b32, twice the LDS cycles)
 __host__ __device__ inline size_t block_lds_bytes(int B, int M) {
-  const size_t keys = 8 * ((size_t)B + 2), cnt = 8 * (size_t)B;
-  return keys + ((cnt + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32 + 4 * (size_t)M;
+  const size_t cnt = 8 * (size_t)B;
+  return ((cnt + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32 + 4 * (size_t)M;
 }
 
-__device__ __forceinline__ BlockLds block_lds(char* base, int B) {
+__device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   BlockLds l;
-  l.key = reinterpret_cast<int2*>(base);
-  char* p = base + 8 * ((size_t)B + 2);
+  l.key = keys;
+  char* p = base;
   l.cnt = reinterpret_cast<int*>(p);
   p += (8 * (size_t)B + 15) & ~(size_t)15;
   l.wt = reinterpret_cast<int*>(p);
@@ -1391,6 +1394,7 @@ template <bool PER_ENV_BS, bool LEAN>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
   extern __shared__ __align__(16) char lds_raw[];
+  __shared__ __align__(16) int2 lds_keys[kMaxB + 2];
   const int u = threadIdx.x;
   const int U = kp.U;
   const int lane = u & 63;
@@ -1399,7 +1403,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const bool valid = u < U;
   const uint64_t lt = (1ull << lane) - 1ull;
   const int M = kp.tab_m;
-  const BlockLds L = block_lds(lds_raw, kp.B);
+  const BlockLds L = block_lds(lds_raw, lds_keys, kp.B);
   for (int e = blockIdx.x; e < kp.E; e += gridDim.x) {
     // ---- prologue: state, stream, station keys, draw table -------------------------------
     const size_t idx = (size_t)e * U + u;
@@ -1534,15 +1538,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // ---- association: min over the env's station keys (LDS broadcast reads) ----------
       unsigned best = UINT_MAX;
       if (active) {
-        const int4* kk2 = reinterpret_cast<const int4*>(L.key);
+        // (an ext_vector_type load: one broadcast ds_read_b128 per two stations; HIP's int4
+        // struct is loaded member-wise, which became four ds_read2_b32 -- twice the LDS cycles)
+        const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
         const int npair = nb >> 1;
         if (scaled) {
           const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
 #pragma unroll 4
           for (int j = 0; j < npair; ++j) {
-            const int4 kv = kk2[j];
-            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), kv.y, false);
-            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.z), kv.w, false);
+            const v4u32 kv = kk2[j];
+            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), (int)kv.y, false);
+            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.z), (int)kv.w, false);
             best = min(best, min(k0, k1));
           }
           if (nb & 1) {
@@ -1553,11 +1559,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           const s16x2 pu = {(short)pos.x, (short)pos.y};
 #pragma unroll 4
           for (int j = 0; j < npair; ++j) {
-            const int4 kv = kk2[j];
+            const v4u32 kv = kk2[j];
             const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.x), 0, true);
             const int d1 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.z), 0, true);
-            best = min(best, min(((unsigned)d0 << kKeyBits) + (unsigned)kv.y,
-                                 ((unsigned)d1 << kKeyBits) + (unsigned)kv.w));
+            best = min(best, min(((unsigned)d0 << kKeyBits) + kv.y, ((unsigned)d1 << kKeyBits) + kv.w));
           }
           if (nb & 1) {
             const int2 kv = L.key[nb - 1];
@@ -1572,7 +1577,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
       const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
       if (srv >= 0) atomicAdd(&cnt[srv], 1);
-      if (!LEAN && lane == 0) L.wt[32 + w] = __popcll(bal(srv >= 0));
+      if (!LEAN) {
+        const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
+        if (lane == 0) L.wt[32 + w] = nc;
+      }
       __syncthreads();  // ---- barrier 2
 
       // ---- C: ResourceFair share + rounding, utility, stores, partial sums -------------

@@ -29,8 +29,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHUNK = 40  # bench.py default --chunk: steps per engine call (rollout launch)
 
-FUSED_RE = re.compile(r"k_steps_packed<")
-SINGLE_RE = re.compile(r"k_step_packed<|k_step_block<(true|false), false>")
+FUSED_RE = re.compile(r"k_steps_packed<|k_steps_block<")
+SINGLE_RE = re.compile(r"k_step_packed<|k_steps_block<")
 
 
 def rows_of(path_glob, name_key):
@@ -92,7 +92,7 @@ def main():
     # counters: per-dispatch averages over the kernel's dispatches of each pass (the fused
     # warmup launches are whole chunks too, so every dispatch is the same work)
     pmc, ndisp = {}, {}
-    for name in ("fetch", "write", "sq", "sq2"):
+    for name in ("fetch", "write", "sq", "sq2", "sq3"):
         vals = {}
         for r in rows_of(os.path.join(out, name, "**", "*counter_collection.csv"), ""):
             if kre.search(r.get("Kernel_Name", "")):
@@ -115,8 +115,12 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "mobile-env-gan_amd"))
         from mobile_env.scenarios.registry import SCENARIOS
         U = SCENARIOS[workload]["num_ues"]
-        pitch = 16 if 8 < U <= 16 and 64 // U == 4 else 32 if 16 < U <= 32 and 64 // U == 2 else U
-        groups = -(-envs // (64 // pitch))
+        if U > 64:  # block shape: one workgroup per env -> counts per env-step
+            groups = envs
+        else:
+            pitch = (16 if 8 < U <= 16 and 64 // U == 4 else
+                     32 if 16 < U <= 32 and 64 // U == 2 else U)
+            groups = -(-envs // (64 // pitch))
         summary["groups_per_launch"] = groups
         summary["valu_per_group_step"] = pmc["SQ_INSTS_VALU"] / groups / steps_per_launch
         summary["salu_per_group_step"] = pmc["SQ_INSTS_SALU"] / groups / steps_per_launch
