@@ -1290,6 +1290,16 @@ __global__ __launch_bounds__(1024) void k_reset_block(KParams kp, KState st, KOu
 // Sum over the 64 lanes of a wavefront (all active), valid in lane 63: row prefix sums by
 // row_shr 1/2/4/8, then the row totals carried by row_bcast:15 (into rows 1, 3) and
 // row_bcast:31 (into rows 2, 3).
+// int16x2 view of a 32-bit word by explicit halves. (__builtin_bit_cast(s16x2, v.z) of an element
+// of a 4 x u32 ext_vector_type load is miscompiled by this LLVM (ROCm 7.2, gfx950): the dot
+// products of both halves of a ds_read_b128 read kv.x -- checked in the generated assembly.)
+__device__ __forceinline__ s16x2 as_s16x2(unsigned v) {
+  s16x2 r;
+  r.x = (short)(v & 0xffffu);
+  r.y = (short)(v >> 16);
+  return r;
+}
+
 __device__ __forceinline__ double wave_sum_f64(double x) {
   x += dpp_f64<0x111>(x);
   x += dpp_f64<0x112>(x);
@@ -1547,26 +1557,26 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 #pragma unroll 4
           for (int j = 0; j < npair; ++j) {
             const v4u32 kv = kk2[j];
-            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), (int)kv.y, false);
-            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.z), (int)kv.w, false);
+            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.x), (int)kv.y, false);
+            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.z), (int)kv.w, false);
             best = min(best, min(k0, k1));
           }
           if (nb & 1) {
             const int2 kv = L.key[nb - 1];
-            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, __builtin_bit_cast(s16x2, kv.x), kv.y, false));
+            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.x), kv.y, false));
           }
         } else {
           const s16x2 pu = {(short)pos.x, (short)pos.y};
 #pragma unroll 4
           for (int j = 0; j < npair; ++j) {
             const v4u32 kv = kk2[j];
-            const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.x), 0, true);
-            const int d1 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.z), 0, true);
+            const int d0 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.x), 0, true);
+            const int d1 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.z), 0, true);
             best = min(best, min(((unsigned)d0 << kKeyBits) + kv.y, ((unsigned)d1 << kKeyBits) + kv.w));
           }
           if (nb & 1) {
             const int2 kv = L.key[nb - 1];
-            const int d0 = __builtin_amdgcn_sdot2(pu, __builtin_bit_cast(s16x2, kv.x), 0, true);
+            const int d0 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.x), 0, true);
             best = min(best, ((unsigned)d0 << kKeyBits) + (unsigned)kv.y);
           }
         }
