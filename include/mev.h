@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 9
+#define MEV_ABI_VERSION 10
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -104,6 +104,22 @@ typedef struct mev_params {
    * with the C library's log10 / pow / log2 in the same order (mev_build_rate_table). */
   const double* rate_table;
   int64_t rate_table_len;
+  /* Heterogeneous entities (entities.py:7-22,33-45: every BaseStation / UserEquipment carries
+   * its own parameters; the channel is evaluated per pair, channels.py:133-146). 0 or 1 classes
+   * on both sides: every station / UE has the bs_* / ue_* / velocity values above. Otherwise
+   * (HOST arrays, read by mev_create only) station j belongs to class bs_class[j] <
+   * num_bs_classes with {bw, freq, tx, height} = bs_class_params[4 c ..], UE u to class
+   * ue_class[u] < num_ue_classes with {velocity, snr_tr, noise, height} = ue_class_params[4 c ..]
+   * (at most 16 classes each); a UE connects to the closest station whose pair SNR exceeds its
+   * snr_tr (base.py:236-241). rate_table then holds one table per class pair
+   * p = cb * num_ue_classes + cu at [rate_table_offsets[p], rate_table_offsets[p + 1]) (NULL
+   * rate_table: built with libm). Heterogeneous contexts run the block kernel for any U. */
+  int32_t num_bs_classes, num_ue_classes;
+  const int32_t* bs_class;
+  const int32_t* ue_class;
+  const double* bs_class_params;
+  const double* ue_class_params;
+  const int64_t* rate_table_offsets;
 } mev_params;
 
 typedef struct mev_state {

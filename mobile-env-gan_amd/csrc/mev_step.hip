@@ -51,6 +51,7 @@ namespace {
 
 constexpr int kMaxU = 1024;
 constexpr int kMaxB = 1024;
+constexpr int kMaxClasses = 16;  // station / UE parameter classes (heterogeneous entities)
 // largest squared distance of a UE (inside the map) to a station (coordinates < 1024)
 constexpr int64_t kD2Top = 2 * 1023 * 1023;
 constexpr int kKeyBits = 10;
@@ -82,6 +83,8 @@ struct KParams {
   int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off, lds_r16_off;  // byte offsets
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
+  int het;            // heterogeneous entities: nb_cls station classes, nu_cls UE classes
+  int nb_cls, nu_cls, bperm;
 };
 
 struct KState {
@@ -117,6 +120,13 @@ __host__ __device__ __forceinline__ KOut out_row(KOut o, int E, int U, int i) {
   return o;
 }
 
+// Movement parameters of one UE class (velocity and the values derived from it on the host).
+struct MoveP {
+  double vel;
+  float vel_f, move_lim;
+  int d2snap, axis_exact;
+};
+
 struct KTables {
   const double* rate_full;  // [d2max + 1]
   const u128* jump;         // [2*(jmax+1)]: {a^k, G(k)} with G(k) = sum_{i<k} a^i
@@ -138,6 +148,14 @@ struct KTables {
   // so full = rate[rank(d2)] with d2 to the serving station: the same float64 values as
   // `assoc`, from four LDS reads instead of one 16-byte gather from L2 per UE and step.
   const int4* lds_blob;
+  // heterogeneous entities (KParams::het): per station class cb / UE class cu
+  const uint8_t* bs_cls;    // [B] class of station j
+  const uint8_t* ue_cls;    // [U] class of UE u
+  const int2* pair;         // [NB * NU] {offset into rate_full, d2max} of class pair cb * NU + cu
+  const MoveP* mv;          // [NU] movement parameters per UE class
+  const int16_t* perm;      // [kp.bperm] stations grouped by class (segments of even length,
+                            // padded with -1)
+  const int* seg;           // [NB + 1] segment bounds in perm
 };
 
 // Element at a 32-bit byte offset from a wave-uniform base: addresses become
@@ -242,35 +260,40 @@ __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel)
 // 2^-16 * max(1, velocity) (30x wider) of a half-integer -- where float32 could pick the
 // other integer, or half-to-even needs the exact value -- is the exact float64 form used. Axis-parallel
 // moves (q = +-velocity exactly) are done exactly in float64 (no division needed).
-template <int SCN = 0>
-__device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
+__device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) {
   const int dx = wp.x - pos.x;
   const int dy = wp.y - pos.y;
   // |dx|, |dy| <= map size < 2^23: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate)
   const int d2 = __mul24(dx, dx) + __mul24(dy, dy);
-  if (d2 <= KPS(d2snap)) {  // arrived: snap to waypoint and pop it
+  if (d2 <= mp.d2snap) {  // arrived: snap to waypoint and pop it
     pos = wp;
     wp = make_int2(-1, -1);
     return;
   }
-  if (KPS(axis_exact) && (dx == 0 || dy == 0)) {
-    const double q = kp.vel;
+  if (mp.axis_exact && (dx == 0 || dy == 0)) {
+    const double q = mp.vel;
     if (dy == 0) pos.x = (int)rint((double)pos.x + (dx > 0 ? q : -q));
     else pos.y = (int)rint((double)pos.y + (dy > 0 ? q : -q));
     return;
   }
-  const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);  // velocity / |v|
+  const float sc = mp.vel_f * __builtin_amdgcn_rsqf((float)d2);  // velocity / |v|
   const float qx = (float)dx * sc;
   const float qy = (float)dy * sc;
   // clear of a tie: |q - rint(q)| < 0.5 - move_band (<=> |frac(q) - 0.5| > move_band, with the
   // rounding shared with the result; q - rint(q) is exact)
   const float rx = rintf(qx), ry = rintf(qy);
-  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < KPSF(move_lim)) {
+  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < mp.move_lim) {
     pos.x += (int)rx;
     pos.y += (int)ry;
   } else {
-    pos = move_exact(pos, dx, dy, kp.vel);
+    pos = move_exact(pos, dx, dy, mp.vel);
   }
+}
+
+// The context's movement parameters (compile-time constants in a scenario instance).
+template <int SCN = 0>
+__device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
+  move_ue_p(pos, wp, MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)});
 }
 
 // BoundedLogUtility.calculateUtility + scaleUtility (utilities.py:44-55).
@@ -1300,6 +1323,39 @@ __device__ __forceinline__ s16x2 as_s16x2(unsigned v) {
   return r;
 }
 
+// Smallest association key over the station pairs [j0, j1) of the LDS key array (two
+// stations per broadcast ds_read_b128): scaled keys dot2(32 p, m) + c, else (dot2(p, m) << 10) + c
+// (see k_steps_block's prologue).
+__device__ __forceinline__ unsigned scan_key_pairs(const v4u32* __restrict__ kk2, int j0, int j1,
+                                                   bool scaled, int2 pos) {
+  unsigned best = UINT_MAX;
+  if (scaled) {
+    const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) {
+      const v4u32 kv = kk2[j];
+      const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.x), (int)kv.y, false);
+      const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.z), (int)kv.w, false);
+      best = min(best, min(k0, k1));
+    }
+  } else {
+    const s16x2 pu = {(short)pos.x, (short)pos.y};
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) {
+      const v4u32 kv = kk2[j];
+      const int d0 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.x), 0, true);
+      const int d1 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.z), 0, true);
+      best = min(best, min(((unsigned)d0 << kKeyBits) + kv.y, ((unsigned)d1 << kKeyBits) + kv.w));
+    }
+  }
+  return best;
+}
+
+// squared distance encoded in an association key of the UE at pos: key - 2^21 + |p|^2
+__device__ __forceinline__ int key_d2(unsigned key, int2 pos) {
+  return (int)(key >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
+}
+
 __device__ __forceinline__ double wave_sum_f64(double x) {
   x += dpp_f64<0x111>(x);
   x += dpp_f64<0x112>(x);
@@ -1400,11 +1456,11 @@ __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& 
 //   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums
 // The per-station counts alternate between two LDS arrays (the next step's array is zeroed
 // in its B phase), so two barriers per step suffice.
-template <bool PER_ENV_BS, bool LEAN>
+template <bool PER_ENV_BS, bool LEAN, bool HET>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
   extern __shared__ __align__(16) char lds_raw[];
-  __shared__ __align__(16) int2 lds_keys[kMaxB + 2];
+  __shared__ __align__(16) int2 lds_keys[kMaxB + 2 + kMaxClasses];
   const int u = threadIdx.x;
   const int U = kp.U;
   const int lane = u & 63;
@@ -1414,6 +1470,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const uint64_t lt = (1ull << lane) - 1ull;
   const int M = kp.tab_m;
   const BlockLds L = block_lds(lds_raw, lds_keys, kp.B);
+  // heterogeneous entities: this UE's class and movement parameters
+  const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
+  const MoveP mp = HET ? tb.mv[cu]
+                       : MoveP{kp.vel, kp.vel_f, kp.move_lim, kp.d2snap, kp.axis_exact};
   for (int e = blockIdx.x; e < kp.E; e += gridDim.x) {
     // ---- prologue: state, stream, station keys, draw table -------------------------------
     const size_t idx = (size_t)e * U + u;
@@ -1436,25 +1496,28 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // ((|p - q|^2 - |p|^2 + 2^21) << 10) | j; otherwise m = -2 q, key = (dot2(p, m) << 10) + c
     const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
     bool in512 = true;
-    int2 q = make_int2(0, 0);
-    if (u < nb) {
-      q = bsx[u];
-      in512 = q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
-    }
-    for (int i = u + blockDim.x; i < nb; i += blockDim.x) {
+    for (int i = u; i < nb; i += blockDim.x) {
       const int2 qq = bsx[i];
       in512 = in512 && qq.x >= 0 && qq.y >= 0 && qq.x < 512 && qq.y < 512;
     }
     if (M)
       for (int k = u; k < M; k += blockDim.x) L.tab[k] = tb.tab_xy[(size_t)e * M + k];
     const bool scaled = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512;
-    for (int i = u; i < nb; i += blockDim.x) {
-      const int2 qq = i == u ? q : bsx[i];
+    // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
+    // and stations beyond the env's count get the key that never wins, m = 0, c = UINT_MAX)
+    const int nslot = HET ? kp.bperm : nb;
+    for (int k = u; k < nslot; k += blockDim.x) {
+      const int i = HET ? (int)tb.perm[k] : k;
+      if (HET && (i < 0 || i >= nb)) {
+        lds_keys[k] = make_int2(0, -1);
+        continue;
+      }
+      const int2 qq = bsx[i];
       const int f = scaled ? -64 : -2;
       const s16x2 m2 = {(short)(f * qq.x), (short)(f * qq.y)};
-      L.key[i] = make_int2(__builtin_bit_cast(int, m2),
-                           (int)(((unsigned)(qq.x * qq.x + qq.y * qq.y + (1 << 21)) << kKeyBits) |
-                                 (unsigned)i));
+      lds_keys[k] = make_int2(__builtin_bit_cast(int, m2),
+                              (int)(((unsigned)(qq.x * qq.x + qq.y * qq.y + (1 << 21)) << kKeyBits) |
+                                    (unsigned)i));
     }
     for (int i = u; i < kp.B; i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
     bool s_ok = true;  // the slot holds the state after the env's last draw
@@ -1543,49 +1606,47 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       } else if (reset && !M && u == U - 1) {  // reset without draws: after the initial pairs
         L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       }
-      if (active) move_ue(pos, wp, kp);
+      if (active) move_ue_p(pos, wp, mp);
 
       // ---- association: min over the env's station keys (LDS broadcast reads) ----------
+      // (ext_vector_type loads: one broadcast ds_read_b128 per two stations; HIP's int4 struct is
+      // loaded member-wise, which became four ds_read2_b32 -- twice the LDS cycles)
+      const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
       unsigned best = UINT_MAX;
-      if (active) {
-        // (an ext_vector_type load: one broadcast ds_read_b128 per two stations; HIP's int4
-        // struct is loaded member-wise, which became four ds_read2_b32 -- twice the LDS cycles)
-        const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
-        const int npair = nb >> 1;
-        if (scaled) {
-          const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
-#pragma unroll 4
-          for (int j = 0; j < npair; ++j) {
-            const v4u32 kv = kk2[j];
-            const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.x), (int)kv.y, false);
-            const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.z), (int)kv.w, false);
-            best = min(best, min(k0, k1));
-          }
-          if (nb & 1) {
-            const int2 kv = L.key[nb - 1];
-            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2(kv.x), kv.y, false));
-          }
-        } else {
-          const s16x2 pu = {(short)pos.x, (short)pos.y};
-#pragma unroll 4
-          for (int j = 0; j < npair; ++j) {
-            const v4u32 kv = kk2[j];
-            const int d0 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.x), 0, true);
-            const int d1 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.z), 0, true);
-            best = min(best, min(((unsigned)d0 << kKeyBits) + kv.y, ((unsigned)d1 << kKeyBits) + kv.w));
-          }
-          if (nb & 1) {
-            const int2 kv = L.key[nb - 1];
-            const int d0 = __builtin_amdgcn_sdot2(pu, as_s16x2(kv.x), 0, true);
-            best = min(best, ((unsigned)d0 << kKeyBits) + (unsigned)kv.y);
+      int srv = -1, d2s = 0;
+      double full = 0.0;
+      if (!HET) {
+        if (active) {
+          best = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos);
+          if (nb & 1) {  // the odd last station
+            const int2 kv = lds_keys[nb - 1];
+            const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
+            const s16x2 pu = {(short)pos.x, (short)pos.y};
+            best = min(best, scaled ? (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false)
+                                    : ((unsigned)__builtin_amdgcn_sdot2(pu, as_s16x2((unsigned)kv.x), 0, true) << kKeyBits) +
+                                          (unsigned)kv.y);
           }
         }
+        d2s = key_d2(best, pos);
+        if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & ((1u << kKeyBits) - 1));
+        full = tb.rate_full[max(0, min(d2s, kp.d2max))];
+      } else {
+        // per station class: the class's closest station, connectable iff d2 <= d2max of the
+        // (station class, this UE's class) pair -- the closest connectable station overall is
+        // the smallest key among the connectable class minima (base.py:236-241)
+        if (active) {
+          for (int c = 0; c < kp.nb_cls; ++c) {
+            const unsigned bc = scan_key_pairs(kk2, tb.seg[c] >> 1, tb.seg[c + 1] >> 1, scaled, pos);
+            if (bc != UINT_MAX && key_d2(bc, pos) <= tb.pair[c * kp.nu_cls + cu].y)
+              best = min(best, bc);
+          }
+        }
+        d2s = key_d2(best, pos);
+        if (best != UINT_MAX) {
+          srv = (int)(best & ((1u << kKeyBits) - 1));
+          full = tb.rate_full[tb.pair[(int)tb.bs_cls[srv] * kp.nu_cls + cu].x + d2s];
+        }
       }
-      // d2 of the best station: key - 2^21 + |p|^2
-      const int d2s = (int)(best >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
-      const int srv =
-          (best != UINT_MAX && d2s <= kp.d2max) ? (int)(best & ((1u << kKeyBits) - 1)) : -1;
-      const double full = tb.rate_full[max(0, min(d2s, kp.d2max))];
       if (srv >= 0) atomicAdd(&cnt[srv], 1);
       if (!LEAN) {
         const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
@@ -1804,6 +1865,13 @@ struct mev_ctx {
   hipStream_t aux;    // second stream of the two-half shape
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
+  // heterogeneous entities (build_het)
+  uint8_t* h_bcl;
+  uint8_t* h_ucl;
+  int2* h_pair;
+  MoveP* h_mv;
+  int16_t* h_perm;
+  int* h_seg;
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -1848,6 +1916,31 @@ static int validate(const mev_params* p) {
     return MEV_EINVAL;
   if (p->rate_table && (p->rate_table_len < 0 || p->rate_table_len > kD2Top + 1))
     return MEV_EINVAL;
+  if (p->num_bs_classes < 0 || p->num_ue_classes < 0 || p->num_bs_classes > kMaxClasses ||
+      p->num_ue_classes > kMaxClasses)
+    return MEV_EINVAL;
+  if (p->num_bs_classes > 1 || p->num_ue_classes > 1) {
+    const int NB = p->num_bs_classes > 1 ? p->num_bs_classes : 1;
+    const int NU = p->num_ue_classes > 1 ? p->num_ue_classes : 1;
+    if ((NB > 1 && (!p->bs_class || !p->bs_class_params)) ||
+        (NU > 1 && (!p->ue_class || !p->ue_class_params)))
+      return MEV_EINVAL;
+    for (int j = 0; NB > 1 && j < p->num_bs; ++j)
+      if (p->bs_class[j] < 0 || p->bs_class[j] >= NB) return MEV_EINVAL;
+    for (int u = 0; NU > 1 && u < p->num_ues; ++u)
+      if (p->ue_class[u] < 0 || p->ue_class[u] >= NU) return MEV_EINVAL;
+    for (int c = 0; NU > 1 && c < NU; ++c)
+      if (!(p->ue_class_params[4 * c] >= 0.0) || !(p->ue_class_params[4 * c + 2] > 0.0))
+        return MEV_EINVAL;
+    if (p->rate_table) {
+      if (!p->rate_table_offsets) return MEV_EINVAL;
+      for (int i = 0; i < NB * NU; ++i)
+        if (p->rate_table_offsets[i] < 0 || p->rate_table_offsets[i + 1] < p->rate_table_offsets[i] ||
+            p->rate_table_offsets[i + 1] > p->rate_table_len ||
+            p->rate_table_offsets[i + 1] - p->rate_table_offsets[i] > kD2Top + 1)
+          return MEV_EINVAL;
+    }
+  }
   return MEV_OK;
 }
 
@@ -2038,6 +2131,129 @@ int64_t mev_build_rate_table(const mev_params* p, double* dst, int64_t cap) {
   return prefix ? n : MEV_ECHANNEL;
 }
 
+// Movement parameters of a velocity (host IEEE float64 == device): the arrival threshold
+// d2snap = largest integer d2 with sqrt(d2) <= velocity, axis-parallel exactness, the float32
+// fast path's velocity and tie band (move_ue_p).
+static MoveP host_move_params(double velocity, int W, int H) {
+  MoveP mp;
+  mp.vel = velocity;
+  mp.vel_f = (float)velocity;
+  const float band = 0x1p-16f * (velocity > 1.0 ? (float)velocity : 1.0f);
+  mp.move_lim = 0.5f - band;
+  const int d2_top = (W - 1) * (W - 1) + (H - 1) * (H - 1);
+  int d2 = 0;
+  while (d2 <= d2_top && sqrt((double)d2) <= velocity) ++d2;
+  mp.d2snap = d2 - 1;
+  mp.axis_exact = 1;
+  const int amax = W > H ? W : H;
+  for (int a = 1; a <= amax; ++a)
+    if ((velocity * (double)a) / (double)a != velocity) mp.axis_exact = 0;
+  return mp;
+}
+
+static bool is_het(const mev_params* p) { return p->num_bs_classes > 1 || p->num_ue_classes > 1; }
+
+// Heterogeneous entities: class arrays, per-pair channel tables (the caller's, else libm per
+// pair), per-UE-class movement parameters, stations grouped by class. Fills c->rate_full and
+// the KTables het pointers; kp.d2max = the largest pair d2max.
+static int build_het(mev_ctx* c) {
+  const mev_params* p = &c->p;
+  KParams& kp = c->kp;
+  const int NB = std::max(1, p->num_bs_classes), NU = std::max(1, p->num_ue_classes);
+  const int B = p->num_bs, U = p->num_ues;
+  std::vector<uint8_t> bcl(B, 0), ucl(U, 0);
+  for (int j = 0; j < B; ++j) bcl[j] = (uint8_t)(p->bs_class ? p->bs_class[j] : 0);
+  for (int u = 0; u < U; ++u) ucl[u] = (uint8_t)(p->ue_class ? p->ue_class[u] : 0);
+  // per-pair tables, concatenated
+  std::vector<double> all;
+  std::vector<int2> pair((size_t)NB * NU);
+  for (int cb = 0; cb < NB; ++cb)
+    for (int cu = 0; cu < NU; ++cu) {
+      const int pi = cb * NU + cu;
+      mev_params q = *p;
+      if (p->bs_class_params) {
+        q.bs_bw = p->bs_class_params[4 * cb];
+        q.bs_freq = p->bs_class_params[4 * cb + 1];
+        q.bs_tx = p->bs_class_params[4 * cb + 2];
+        q.bs_height = p->bs_class_params[4 * cb + 3];
+      }
+      if (p->ue_class_params) {
+        q.ue_snr_tr = p->ue_class_params[4 * cu + 1];
+        q.ue_noise = p->ue_class_params[4 * cu + 2];
+        q.ue_height = p->ue_class_params[4 * cu + 3];
+      }
+      int64_t n;
+      const size_t off = all.size();
+      if (p->rate_table) {
+        const int64_t a = p->rate_table_offsets[pi], b = p->rate_table_offsets[pi + 1];
+        n = b - a;
+        all.insert(all.end(), p->rate_table + a, p->rate_table + b);
+      } else {
+        n = mev_build_rate_table(&q, nullptr, 0);
+        if (n < 0) return (int)n;
+        all.resize(off + (size_t)n);
+        if (n) (void)mev_build_rate_table(&q, all.data() + off, n);
+      }
+      pair[pi] = make_int2((int)off, (int)n - 1);
+      kp.d2max = std::max(kp.d2max, (int)n - 1);
+    }
+  all.push_back(0.0);  // (never indexed; keeps the buffer non-empty)
+  std::vector<MoveP> mv(NU);
+  for (int cu = 0; cu < NU; ++cu)
+    mv[cu] = host_move_params(p->ue_class_params ? p->ue_class_params[4 * cu] : p->velocity,
+                              p->width, p->height);
+  // stations grouped by class, each segment padded to an even length (pairs of keys)
+  std::vector<int16_t> perm;
+  std::vector<int> seg(NB + 1, 0);
+  for (int cb = 0; cb < NB; ++cb) {
+    seg[cb] = (int)perm.size();
+    for (int j = 0; j < B; ++j)
+      if (bcl[j] == cb) perm.push_back((int16_t)j);
+    if (perm.size() & 1) perm.push_back(-1);
+  }
+  seg[NB] = (int)perm.size();
+  kp.het = 1;
+  kp.nb_cls = NB;
+  kp.nu_cls = NU;
+  kp.bperm = (int)perm.size();
+  if (hipMalloc(&c->rate_full, sizeof(double) * all.size()) != hipSuccess ||
+      hipMalloc(&c->h_bcl, (size_t)B) != hipSuccess || hipMalloc(&c->h_ucl, (size_t)U) != hipSuccess ||
+      hipMalloc(&c->h_pair, sizeof(int2) * pair.size()) != hipSuccess ||
+      hipMalloc(&c->h_mv, sizeof(MoveP) * mv.size()) != hipSuccess ||
+      hipMalloc(&c->h_perm, sizeof(int16_t) * std::max<size_t>(perm.size(), 1)) != hipSuccess ||
+      hipMalloc(&c->h_seg, sizeof(int) * seg.size()) != hipSuccess)
+    return MEV_ENOMEM;
+  MEV_HIP(hipMemcpy(c->rate_full, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice));
+  MEV_HIP(hipMemcpy(c->h_bcl, bcl.data(), (size_t)B, hipMemcpyHostToDevice));
+  MEV_HIP(hipMemcpy(c->h_ucl, ucl.data(), (size_t)U, hipMemcpyHostToDevice));
+  MEV_HIP(hipMemcpy(c->h_pair, pair.data(), sizeof(int2) * pair.size(), hipMemcpyHostToDevice));
+  MEV_HIP(hipMemcpy(c->h_mv, mv.data(), sizeof(MoveP) * mv.size(), hipMemcpyHostToDevice));
+  if (!perm.empty())
+    MEV_HIP(hipMemcpy(c->h_perm, perm.data(), sizeof(int16_t) * perm.size(), hipMemcpyHostToDevice));
+  MEV_HIP(hipMemcpy(c->h_seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice));
+  c->d2max = kp.d2max;
+  return MEV_OK;
+}
+
+static KTables tables_of(const mev_ctx* c) {
+  KTables tb{};
+  tb.rate_full = c->rate_full;
+  tb.jump = c->jump;
+  tb.util = c->util;
+  tb.assoc = c->assoc;
+  tb.tab_xy = c->tab_xy;
+  tb.tab_st = c->tab_st;
+  tb.drawn = c->drawn;
+  tb.lds_blob = c->blob;
+  tb.bs_cls = c->h_bcl;
+  tb.ue_cls = c->h_ucl;
+  tb.pair = c->h_pair;
+  tb.mv = c->h_mv;
+  tb.perm = c->h_perm;
+  tb.seg = c->h_seg;
+  return tb;
+}
+
 int mev_create(const mev_params* params, mev_ctx** out) {
   if (!out) return MEV_EINVAL;
   *out = nullptr;
@@ -2082,23 +2298,17 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.u_upperf = (float)kp.upper;
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
-  kp.vel_f = (float)params->velocity;
   {
     const char* xr = getenv("MEV_XCD_REMAP");  // dev A/B switch
     kp.xcd_remap = xr ? atoi(xr) : 1;
   }
-  kp.move_band = 0x1p-16f * (params->velocity > 1.0 ? (float)params->velocity : 1.0f);
-  kp.move_lim = 0.5f - kp.move_band;
-  {  // arrival threshold and axis-parallel exactness (host IEEE float64 == device)
-    const int d2_top = (params->width - 1) * (params->width - 1) +
-                       (params->height - 1) * (params->height - 1);
-    int d2 = 0;
-    while (d2 <= d2_top && sqrt((double)d2) <= params->velocity) ++d2;
-    kp.d2snap = d2 - 1;
-    kp.axis_exact = 1;
-    const int amax = params->width > params->height ? params->width : params->height;
-    for (int a = 1; a <= amax; ++a)
-      if ((params->velocity * (double)a) / (double)a != params->velocity) kp.axis_exact = 0;
+  {
+    const MoveP mp = host_move_params(params->velocity, params->width, params->height);
+    kp.vel_f = mp.vel_f;
+    kp.move_lim = mp.move_lim;
+    kp.move_band = 0.5f - mp.move_lim;
+    kp.d2snap = mp.d2snap;
+    kp.axis_exact = mp.axis_exact;
   }
   // utility saturation point r_sat = w3^(upper/w1) - w2 (increasing utility only)
   kp.util_direct = 1;
@@ -2113,7 +2323,14 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   }
 
   // ---- channel table: the caller's (numpy, Python host), else built here with libm ----
-  {
+  if (is_het(params)) {
+    c->kp.d2max = -1;
+    rc = build_het(c);
+    if (rc) {
+      mev_destroy(c);
+      return rc;
+    }
+  } else {
     std::vector<double> host;
     const double* tab = params->rate_table;
     int64_t n = params->rate_table_len;
@@ -2172,7 +2389,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   // ---- association map of a shared layout (filled by mev_reset / mev_update_stations;
   //      <= 1024 x 1024 x 16 B)
   c->assoc = nullptr;
-  if (!params->bs_per_env) {
+  if (!params->bs_per_env && !c->kp.het) {
     const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height;
     if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
       mev_destroy(c);
@@ -2238,6 +2455,9 @@ void mev_destroy(mev_ctx* c) {
   if (c->tab_xy) (void)hipFree(c->tab_xy);
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
+  for (void* h : {(void*)c->h_bcl, (void*)c->h_ucl, (void*)c->h_pair, (void*)c->h_mv,
+                  (void*)c->h_perm, (void*)c->h_seg})
+    if (h) (void)hipFree(h);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -2405,8 +2625,10 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
   const bool per_env = c->p.bs_per_env != 0;
   void (*kf)(KParams, KState, KOut, KTables, int, int) =
-      per_env ? (lean ? k_steps_block<true, true> : k_steps_block<true, false>)
-              : (lean ? k_steps_block<false, true> : k_steps_block<false, false>);
+      kp.het ? (per_env ? (lean ? k_steps_block<true, true, true> : k_steps_block<true, false, true>)
+                        : (lean ? k_steps_block<false, true, true> : k_steps_block<false, false, true>))
+             : (per_env ? (lean ? k_steps_block<true, true, false> : k_steps_block<true, false, false>)
+                        : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
   const size_t shm = block_lds_bytes(kp.B, kp.tab_m);
   if (c->fuse_steps || nsteps == 1) {
@@ -2426,10 +2648,9 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
-             c->blob};
+  const KTables tb = tables_of(c);
   const KParams& kp = c->kp;
-  if (kp.U <= 64) {
+  if (kp.U <= 64 && !kp.het) {
     const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
     if (RESET) {
       const dim3 grid((unsigned)((groups + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -2450,7 +2671,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
 
 int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   if (!c || !bs_xy) return MEV_EINVAL;
-  if (c->p.bs_per_env) return MEV_OK;  // per-env layouts are read directly by the kernel
+  if (c->p.bs_per_env || c->kp.het) return MEV_OK;  // the block kernel reads bs_xy itself
   const int cells = c->p.width * c->p.height;
   hipLaunchKernelGGL(k_assoc_map, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
@@ -2498,9 +2719,9 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
   KState ks;
   KOut ko;
   to_kernel(st, out, ks, ko);
-  const KTables tb{c->rate_full, c->jump, c->util, c->assoc, c->tab_xy, c->tab_st, c->drawn,
-                   c->blob};
-  if (c->kp.U <= 64) return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
+  const KTables tb = tables_of(c);
+  if (c->kp.U <= 64 && !c->kp.het)
+    return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
   return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
 }
 

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -45,6 +45,10 @@ class MevParams(C.Structure):
         ("util_w1", C.c_double), ("util_w2", C.c_double), ("util_w3", C.c_double),
         ("qoe_low", C.c_double),
         ("rate_table", C.c_void_p), ("rate_table_len", C.c_int64),
+        ("num_bs_classes", C.c_int32), ("num_ue_classes", C.c_int32),
+        ("bs_class", C.c_void_p), ("ue_class", C.c_void_p),
+        ("bs_class_params", C.c_void_p), ("ue_class_params", C.c_void_p),
+        ("rate_table_offsets", C.c_void_p),
     ]
 
 

@@ -252,9 +252,9 @@ class MComCore:
         return self.time >= min(self.EP_MAX_TIME, self.max_departure)
 
     def check_connectivity(self, bs: BaseStation, ue: UserEquipment) -> bool:
-        """snr > snr_tr, which the device channel table reduces to d2 <= d2max."""
-        d = bs.point.x - ue.point.x, bs.point.y - ue.point.y
-        return d[0] * d[0] + d[1] * d[1] <= self._ensure_engine().d2max
+        """base.py:212-214: snr > snr_tr, by the channel plugin (the step's kernels use the
+        equivalent integer test d2 <= d2max of the pair's parameter classes)."""
+        return self.channelModel.calculateSNR(bs, ue) > ue.snr_threshold
 
     def available_connections(self, ue: UserEquipment) -> Set:
         return {bs for bs in self.stationDict.values() if self.check_connectivity(bs, ue)}

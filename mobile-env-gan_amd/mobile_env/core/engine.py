@@ -56,20 +56,69 @@ class EngineParams:
     draw_table: int = -1   # mev_params.draw_table: episode draw table pairs per env (-1 auto)
     fuse_steps: int = 0    # mev_params.fuse_steps: 0 step(n > 1) in one launch, -1 n launches
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
+    # heterogeneous entities (entities.py:7-22,33-45): parameter classes and each station's /
+    # UE's class (None: every entity has bs / ue / velocity above); see lowering.lower
+    bs_classes: "list | None" = None   # [{bw, freq, tx, height}]
+    ue_classes: "list | None" = None   # [{velocity, snr_tr, noise, height}]
+    bs_class: "list | None" = None     # [B] class index per station
+    ue_class: "list | None" = None     # [U] class index per UE
+
+    @property
+    def heterogeneous(self) -> bool:
+        return len(self.bs_classes or ()) > 1 or len(self.ue_classes or ()) > 1
+
+    def _classes(self):
+        bsc = self.bs_classes or [dict(self.bs)]
+        uec = self.ue_classes or [dict(self.ue, velocity=self.velocity)]
+        return bsc, uec
 
     def rate_table(self):
-        """The channel rate table of these parameters (numpy, reference op order; see
-        mobile_env.core.channels): float64 [d2max + 1]."""
+        """The channel rate table(s) of these parameters (numpy, reference op order; see
+        mobile_env.core.channels): float64 [d2max + 1]; heterogeneous entities: one table per
+        (station class, UE class) pair concatenated, and the [NB * NU + 1] offsets."""
+        import numpy as np
         from .channels import OkumuraHata
-        return OkumuraHata().rate_table(self.bs, self.ue, int(self.width), int(self.height))
+        W, H = int(self.width), int(self.height)
+        if not self.heterogeneous:
+            return OkumuraHata().rate_table(self.bs, self.ue, W, H)
+        bsc, uec = self._classes()
+        tabs = [OkumuraHata().rate_table(b, u, W, H) for b in bsc for u in uec]
+        offs = np.concatenate([[0], np.cumsum([len(t) for t in tabs])]).astype(np.int64)
+        return np.concatenate(tabs).astype(np.float64), offs
 
     def to_c(self, bs_per_env: bool, rate_table=None) -> N.MevParams:
-        """mev_params; ``rate_table`` (float64 numpy array, kept alive by the caller until
-        mev_create returns) is passed as mev_params.rate_table."""
-        tab = (C.c_void_p(rate_table.ctypes.data), len(rate_table)) if rate_table is not None \
+        """mev_params; ``rate_table`` (rate_table()'s result) is passed as mev_params.rate_table.
+        The host arrays the struct points to are kept on the returned struct (``_keep``) until
+        it is dropped: keep it alive until mev_create returns."""
+        import numpy as np
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+            keep.append(a)
+            return C.c_void_p(a.ctypes.data)
+
+        offs = None
+        if isinstance(rate_table, tuple):
+            rate_table, offs = rate_table
+        tab = (arr(rate_table, np.float64), len(rate_table)) if rate_table is not None \
             else (C.c_void_p(None), 0)
-        return N.MevParams(
-            rate_table=tab[0], rate_table_len=tab[1],
+        het = {}
+        if self.heterogeneous:
+            bsc, uec = self._classes()
+            het = dict(
+                num_bs_classes=len(bsc), num_ue_classes=len(uec),
+                bs_class=arr(self.bs_class if self.bs_class is not None
+                             else [0] * self.num_bs, np.int32),
+                ue_class=arr(self.ue_class if self.ue_class is not None
+                             else [0] * self.num_ues, np.int32),
+                bs_class_params=arr([[b["bw"], b["freq"], b["tx"], b["height"]] for b in bsc],
+                                    np.float64),
+                ue_class_params=arr([[u["velocity"], u["snr_tr"], u["noise"], u["height"]]
+                                     for u in uec], np.float64),
+                rate_table_offsets=arr(offs, np.int64) if offs is not None else C.c_void_p(None))
+        cp = N.MevParams(
+            rate_table=tab[0], rate_table_len=tab[1], **het,
             num_envs=self.num_envs, num_ues=self.num_ues, num_bs=self.num_bs,
             width=int(self.width), height=int(self.height), ep_max_time=int(self.ep_max_time),
             arrival_start=int(self.arrival_start), arrival_exit=int(self.arrival_exit),
@@ -85,6 +134,8 @@ class EngineParams:
             util_lower=float(self.util_lower), util_upper=float(self.util_upper),
             util_w1=float(self.util_coeffs[0]), util_w2=float(self.util_coeffs[1]),
             util_w3=float(self.util_coeffs[2]), qoe_low=float(self.qoe_low))
+        cp._keep = keep
+        return cp
 
     @property
     def t_end(self) -> int:

@@ -55,34 +55,43 @@ def check_plugins(arrival, channel, scheduler, movement, utility):
                 f"only")
 
 
-def _uniform(values, what):
-    vals = list(values)
-    if not vals:
-        raise ValueError(f"no {what}")
-    first = vals[0]
-    for v in vals[1:]:
-        if v != first:
-            raise NotImplementedError(
-                f"per-entity {what} parameters differ ({first} vs {v}); the engine lowers one "
-                f"parameter set per batch")
-    return first
+def _classes(values):
+    """(distinct values in order of first appearance, class index of every entity)."""
+    classes, index = [], []
+    for v in values:
+        if v not in classes:
+            classes.append(v)
+        index.append(classes.index(v))
+    if not classes:
+        raise ValueError("no entities")
+    return classes, index
 
 
 def lower(*, num_envs, stations, users, arrival, channel, scheduler, movement, utility,
           ep_max_time, first_step_active) -> EngineParams:
+    """Flat engine parameters. Entities with different parameters (the reference keeps them
+    per BaseStation / UserEquipment, entities.py:7-22,33-45) lower to parameter classes: one
+    channel table per (station class, UE class) pair and the movement velocity per UE class."""
     check_plugins(arrival, channel, scheduler, movement, utility)
-    bsp = _uniform(((s.bw, s.frequency, s.tx_power, s.height) for s in stations), "station")
-    uep = _uniform(((u.velocity, u.snr_threshold, u.noise, u.height) for u in users), "UE")
+    bsc, bsi = _classes([(s.bw, s.frequency, s.tx_power, s.height) for s in stations])
+    uec, uei = _classes([(u.velocity, u.snr_threshold, u.noise, u.height) for u in users])
+    if len(bsc) > 16 or len(uec) > 16:
+        raise NotImplementedError("more than 16 station or UE parameter classes")
     mv = movement.lower_params()
     ar = arrival.lower_params()
     ut = utility.lower_params()
+    bs_dicts = [{"bw": b[0], "freq": b[1], "tx": b[2], "height": b[3]} for b in bsc]
+    ue_dicts = [{"velocity": float(u[0]), "snr_tr": u[1], "noise": u[2], "height": u[3]}
+                for u in uec]
+    het = len(bsc) > 1 or len(uec) > 1
     return EngineParams(
         num_envs=num_envs, num_ues=len(users), num_bs=len(stations),
         width=mv["width"], height=mv["height"], ep_max_time=int(ep_max_time),
         arrival_start=ar["arrival_start"], arrival_exit=ar["arrival_exit"],
         first_step_active=first_step_active, movement_reseed=mv["movement_reseed"],
-        velocity=float(uep[0]),
-        bs={"bw": bsp[0], "freq": bsp[1], "tx": bsp[2], "height": bsp[3]},
-        ue={"snr_tr": uep[1], "noise": uep[2], "height": uep[3]},
+        velocity=float(uec[0][0]), bs=bs_dicts[0],
+        ue={k: ue_dicts[0][k] for k in ("snr_tr", "noise", "height")},
         util_lower=ut["util_lower"], util_upper=ut["util_upper"], util_coeffs=ut["util_coeffs"],
-        draw_table=0)  # the facade carries pcg / t across engine rebuilds: no episode table
+        draw_table=0,  # the facade carries pcg / t across engine rebuilds: no episode table
+        bs_classes=bs_dicts if het else None, ue_classes=ue_dicts if het else None,
+        bs_class=bsi if het else None, ue_class=uei if het else None)

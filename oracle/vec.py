@@ -40,6 +40,12 @@ class OracleParams:
     lower: float = -20             # base.py:136
     upper: float = 20
     coeffs: tuple = (10, 0, 10)
+    # heterogeneous entities (entities.py:7-22,33-45): per-station / per-UE parameter classes
+    # ({bw, freq, tx, height} / {velocity, snr_tr, noise, height}) and each entity's class
+    bs_classes: list = None
+    ue_classes: list = None
+    bs_class: list = None
+    ue_class: list = None
 
     @property
     def t_end(self) -> int:
@@ -94,6 +100,28 @@ class OracleBatch:
                          else np.asarray(bs_count, dtype=np.int64).reshape(-1))
         self.U = int(num_ues)
         self.d2max, self.rate_full = table if table is not None else channel_table(p)
+        # per (station, UE) pair: its class pair's d2max and table (one pair when homogeneous);
+        # the velocity per UE
+        self.vel = np.full(self.U, float(p.velocity))
+        self.pair_d2max = np.full((self.B, self.U), self.d2max, dtype=np.int64)
+        self.pair_id = np.zeros((self.B, self.U), dtype=np.int64)
+        self.tables = [self.rate_full]
+        if p.bs_classes is not None or p.ue_classes is not None:
+            bsc = p.bs_classes or [p.bs]
+            uec = p.ue_classes or [dict(p.ue, velocity=p.velocity)]
+            bcl = np.asarray(p.bs_class if p.bs_class is not None else [0] * self.B)
+            ucl = np.asarray(p.ue_class if p.ue_class is not None else [0] * self.U)
+            d2m, self.tables = [], []
+            for b in bsc:
+                for u in uec:
+                    q = OracleParams(width=p.width, height=p.height, bs=dict(b),
+                                     ue={k: u[k] for k in ("snr_tr", "noise", "height")})
+                    dm, tab = channel_table(q)
+                    d2m.append(dm)
+                    self.tables.append(tab)
+            self.pair_id = bcl[:, None] * len(uec) + ucl[None, :]
+            self.pair_d2max = np.asarray(d2m, dtype=np.int64)[self.pair_id]
+            self.vel = np.asarray([float(uec[c]["velocity"]) for c in ucl])
         self.t = np.full(self.E, p.t_end, dtype=np.int64)   # "episode over": next step resets
         self.x = np.zeros((self.E, self.U), dtype=np.int64)
         self.y = np.zeros((self.E, self.U), dtype=np.int64)
@@ -128,7 +156,8 @@ class OracleBatch:
         if len(lazy):
             self.reset(lazy)
         t = self.t
-        W, H, vel = p.width, p.height, p.velocity
+        W, H = p.width, p.height
+        vel = self.vel[None, :]
         # NoDeparture: start 0, exit arrival_ep_time; active during step t iff start <= t < exit
         active = np.broadcast_to(((t >= 0) & (t < p.arrival_ep_time))[:, None],
                                  (self.E, self.U)).copy()
@@ -158,7 +187,7 @@ class OracleBatch:
         by = self.bs_xy[:, None, :, 1]
         d2 = (self.x[:, :, None] - bx) ** 2 + (self.y[:, :, None] - by) ** 2      # [E,U,B]
         valid_bs = np.arange(self.B)[None, None, :] < self.bs_count[:, None, None]
-        conn = (d2 <= self.d2max) & valid_bs & active[:, :, None]
+        conn = (d2 <= self.pair_d2max.T[None]) & valid_bs & active[:, :, None]
         big = np.iinfo(np.int64).max
         srv = np.argmin(np.where(conn, d2, big), axis=2)
         has = conn.any(axis=2)
@@ -170,7 +199,13 @@ class OracleBatch:
         for b in range(self.B):
             nb[:, b] = (serving == b).sum(axis=1)
         n = np.take_along_axis(nb, np.maximum(serving, 0), axis=1)
-        full = self.rate_full[np.where(has, d2s, 0)]
+        if len(self.tables) == 1:
+            full = self.rate_full[np.where(has, d2s, 0)]
+        else:  # the serving pair's class-pair table
+            pid = self.pair_id.T[np.arange(self.U)[None, :], np.maximum(serving, 0)]
+            full = np.array([self.tables[k][d] if h else 0.0
+                             for k, d, h in zip(pid.ravel(), d2s.ravel(), has.ravel())]
+                            ).reshape(d2s.shape)
         share = np.where(has, full / np.maximum(n, 1), 0.0)
         rate = np.where(has, np.round(share, 2), 0.0)
 

@@ -144,3 +144,33 @@ def test_make_custom_layouts_are_the_fixture_layouts():
         np.testing.assert_allclose(rew.cpu().numpy(), d["metrics"][:, s, 2], rtol=1e-5,
                                    atol=1e-7)
     env.close()
+
+
+def test_mcom_core_facade_heterogeneous_entities():
+    """MComCore over stations / UEs that carry their own parameters (the reference's entity
+    model, entities.py:7-45): the facade lowers them to parameter classes and reproduces the
+    reference's heterogeneous fixture."""
+    import json
+    from mobile_env.core.base import MComCore
+    from mobile_env.core.entities import BaseStation, UserEquipment
+    d = load("large_mixed")
+    bsc, uec = json.loads(str(d["bs_classes"])), json.loads(str(d["ue_classes"]))
+
+    class Core(MComCore):
+        _first_step_active = True  # the fixture's driver refills activeUsers at reset
+
+    for k, seed in enumerate(d["seeds"]):
+        st = [BaseStation(j, (int(x), int(y)), **bsc[c])
+              for j, ((x, y), c) in enumerate(zip(d["bs_xy"], d["bs_class"]))]
+        us = [UserEquipment(i, **uec[c]) for i, c in enumerate(d["ue_class"])]
+        env = Core(st, us, {"seed": int(seed)})
+        for ep in range(2):
+            env.reset()
+            env.activeUsers = sorted(us, key=lambda u: u.ue_id)
+            for s in range(20):
+                env.step(ep, s)
+                assert [[int(u.x), int(u.y)] for u in us] == d["xy"][k, ep * 20 + s].tolist()
+                rates = [float(env.allUserDataRates.get(u, 0.0)) for u in us]
+                assert rates == d["rate"][k, ep * 20 + s].tolist()
+        assert env.check_connectivity(st[0], us[0]) in (True, False)
+        env.close()

@@ -154,10 +154,16 @@ def test_lowering_builtin_plugins_and_rejects_others():
     with pytest.raises(NotImplementedError):
         lowering.check_plugins(plug["arrival"], LossyHata(), plug["scheduler"],
                                plug["movement"], plug["utility"])
+    # entities with their own parameters lower to parameter classes (entities.py:7-22,33-45)
     us[2].velocity = 3.0
-    with pytest.raises(NotImplementedError):
-        lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
+    st[1].tx_power = 30
+    p = lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
                        first_step_active=True, **plug)
+    assert p.heterogeneous and p.bs_class == [0, 1, 0] and p.ue_class == [0, 0, 1, 0]
+    assert [c["tx"] for c in p.bs_classes] == [40, 30]
+    assert [c["velocity"] for c in p.ue_classes] == [1.5, 3.0]
+    tab, offs = p.rate_table()
+    assert len(offs) == 2 * 2 + 1 and offs[-1] == len(tab)
 
 
 def test_mcom_custom_layout_uses_global_random_like_reference():

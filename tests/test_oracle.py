@@ -153,3 +153,28 @@ def test_velocity_int_and_float_agree():
     # MComCustom uses an int velocity (custom.py:17); int*v and float*v give the same step
     d = 37
     assert (10 * d) / math.sqrt(d * d) == (10.0 * d) / math.sqrt(d * d)
+
+
+def _mixed_oracle(d):
+    import json
+    bsc, uec = json.loads(str(d["bs_classes"])), json.loads(str(d["ue_classes"]))
+    p = OracleParams(bs_classes=bsc, ue_classes=uec, bs_class=d["bs_class"].tolist(),
+                     ue_class=d["ue_class"].tolist())
+    return OracleBatch(p, d["bs_xy"], d["xy"].shape[2], d["seeds"])
+
+
+def test_vec_oracle_matches_heterogeneous_fixture():
+    """Per-station (bw, freq, tx, height) and per-UE (velocity, snr_tr, noise, height)
+    parameters (entities.py:7-22,33-45; the reference evaluates the channel per pair,
+    channels.py:133-146): the oracle with one table per class pair and per-UE velocities
+    reproduces the reference's positions, serving stations, rates and utilities bit for bit."""
+    d = load("large_mixed")
+    ob = _mixed_oracle(d)
+    for s in range(d["xy"].shape[1]):
+        o = ob.step()
+        np.testing.assert_array_equal(o["xy"], d["xy"][:, s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(o["serving"], d["serving"][:, s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(o["rate"], d["rate"][:, s], err_msg=f"step {s}")
+        act = ~np.isnan(d["util"][:, s])
+        np.testing.assert_array_equal(o["util"][act], d["util"][:, s][act])
+        np.testing.assert_array_equal(o["metrics"][:, :3], d["metrics"][:, s, :3])
