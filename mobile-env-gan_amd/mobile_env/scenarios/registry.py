@@ -25,6 +25,12 @@ for _size in ("small", "medium", "large"):
 # custom 128 BS x 1024 UE Okumura-Hata stress scenario: one random BS layout per env
 # (uniform integer positions in the 200x200 map, seeded by the env's seed), velocity 10
 # as in MComCustom (custom.py:16-18).
+# mobile-large sizes (13 BS x 30 UE) with one random station layout per env (uniform integer
+# positions, seeded by the env's seed): the per-env-layout path of the packed kernels (the
+# UE x station distance scan; MComCustom and layout search run it).
+SCENARIOS["mobile-large-perenv-v0"] = dict(
+    layout=None, mode="central", num_ues=LAYOUTS["large"]["num_ues"],
+    num_bs=len(LAYOUTS["large"]["bs"]), velocity=None, per_env_layout=True)
 SCENARIOS["mobile-custom-128x1024-v0"] = dict(
     layout=None, mode="central", num_ues=1024, num_bs=128, velocity=10,
     per_env_layout=True)
