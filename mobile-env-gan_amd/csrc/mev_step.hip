@@ -83,6 +83,7 @@ struct KParams {
   int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off, lds_r16_off;  // byte offsets
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
+  int lbs;            // fused per-env-layout launches: station slots per env staged in LDS (0: off)
   int het;            // heterogeneous entities: nb_cls station classes, nu_cls UE classes
   int nb_cls, nu_cls, bperm;
 };
@@ -579,6 +580,16 @@ typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 // s_waitcnt vmcnt(0) only (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait on those)
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// int16x2 view of a 32-bit word by explicit halves. (__builtin_bit_cast(s16x2, v.z) of an element
+// of a 4 x u32 ext_vector_type load is miscompiled by this LLVM (ROCm 7.2, gfx950): the dot
+// products of both halves of a ds_read_b128 read kv.x -- checked in the generated assembly.)
+__device__ __forceinline__ s16x2 as_s16x2(unsigned v) {
+  s16x2 r;
+  r.x = (short)(v & 0xffffu);
+  r.y = (short)(v >> 16);
+  return r;
+}
+
 // Lane mask of a bool: the ballot builtin on the i1 itself (HIP's __ballot takes an int, and
 // the compiler then materialises compound conditions as v_cndmask + v_cmp before the ballot)
 __device__ __forceinline__ uint64_t bal(bool c) { return __builtin_amdgcn_ballot_w64(c); }
@@ -663,7 +674,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                                              u128* __restrict__ lpcg = nullptr,
                                              float* __restrict__ srew = nullptr,
                                              uint8_t* __restrict__ sdone = nullptr,
-                                             uint64_t envok_wf = 0, uint64_t valid_wf = 0) {
+                                             uint64_t envok_wf = 0, uint64_t valid_wf = 0,
+                                             const int* __restrict__ lbs = nullptr,
+                                             int nb_f = 0) {
   constexpr int PC = UC ? pitch_of(UC) : 0;
   constexpr bool ROWS = PC == 16 || PC == 32;  // aligned segments (DPP row reductions)
   constexpr bool LDSA = LDSM != 0;
@@ -827,9 +840,30 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     // index, as python's min() over the station dict)
     unsigned best = UINT_MAX;
     const s16x2 pu = {(short)pos.x, (short)pos.y};
-    const int nb = st.bs_count ? (valid ? st.bs_count[e] : 0) : KPS(B);
+    const bool staged = FUSED && (SCN ? 0 : kp.lbs) != 0;  // (uniform)
+    const int nb = staged ? nb_f : st.bs_count ? (valid ? st.bs_count[e] : 0) : KPS(B);
     const int2* bs = st.bs_xy + (size_t)e * KPS(B);
-    if (active && nb > 0) {
+    if (staged) {
+      // the env's stations from its LDS slots (staged once per launch, 4 per ds_read_b128;
+      // slots past the env's count hold its last station again -- same d2, larger index: the
+      // original wins, as python's min keeps the first)
+      if (active && nb > 0) {
+        const v4u32* sv = reinterpret_cast<const v4u32*>(lbs + m.seg * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q * 4 >= KPS(B)) break;
+          const v4u32 w = sv[q];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int j = q * 4 + i;
+            if (j >= KPS(B)) break;
+            const s16x2 d = pu - as_s16x2(w[i]);  // coordinates < 1024
+            const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
+            best = min(best, (d2 << kKeyBits) | (unsigned)j);
+          }
+        }
+      }
+    } else if (active && nb > 0) {
       const int nb8 = (KPS(B) + 7) & ~7;  // wave-uniform trip count; j clamped to the last
       for (int b0 = 0; b0 < nb8; b0 += 8) {
 #pragma unroll
@@ -1183,7 +1217,9 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   // uniform over the workgroup (its barriers): waves past the last group only take part in them.
   constexpr bool STG = LDSM == 2 && LEAN && UC != 0;
   constexpr int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
-  float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m)));
+  int* lbs = lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m)) + wv * G * (SCN ? 0 : kp.lbs);
+  float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m) +
+                                                              (SCN ? 0 : kp.lbs)));
   uint8_t* sdone = reinterpret_cast<uint8_t*>(srew + (STG ? stage_rows * NWG : 0));
   const int gstride = LDSA ? (int)gridDim.x * NW : ngroups;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -1207,6 +1243,18 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
         if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
     }
     GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
+    // per-env layouts: the env's station count and its stations in the wave's LDS slots
+    int nb_f = 0;
+    if (PER_ENV_BS && (SCN ? 0 : kp.lbs)) {
+      const int ec = min(e, kp.E - 1);
+      nb_f = st.bs_count ? st.bs_count[ec] : KPS(B);
+      if (m.seg < G)  // (lanes past the last segment hold no env)
+        for (int k = m.u; k < 16; k += P) {
+          const int2 q = st.bs_xy[(size_t)ec * KPS(B) + max(0, min(k, nb_f - 1))];
+          lbs[m.seg * 16 + k] = (int)(((unsigned)q.x & 0xffffu) | ((unsigned)q.y << 16));
+        }
+      if (!env_ok) nb_f = 0;
+    }
     const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
     ulonglong2 pa = make_ulonglong2(0, 0), pb = pa;
     if (env_ok && leader) {
@@ -1235,7 +1283,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
       const int sr = STG ? i % stage_rows : 0;
       moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG>(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, lblob, lpcg,
-          srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w);
+          srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w, lbs, nb_f);
       if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
         flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1);
     }
@@ -1313,15 +1361,6 @@ __global__ __launch_bounds__(1024) void k_reset_block(KParams kp, KState st, KOu
 // Sum over the 64 lanes of a wavefront (all active), valid in lane 63: row prefix sums by
 // row_shr 1/2/4/8, then the row totals carried by row_bcast:15 (into rows 1, 3) and
 // row_bcast:31 (into rows 2, 3).
-// int16x2 view of a 32-bit word by explicit halves. (__builtin_bit_cast(s16x2, v.z) of an element
-// of a 4 x u32 ext_vector_type load is miscompiled by this LLVM (ROCm 7.2, gfx950): the dot
-// products of both halves of a ds_read_b128 read kv.x -- checked in the generated assembly.)
-__device__ __forceinline__ s16x2 as_s16x2(unsigned v) {
-  s16x2 r;
-  r.x = (short)(v & 0xffffu);
-  r.y = (short)(v >> 16);
-  return r;
-}
 
 // Smallest association key over the station pairs [j0, j1) of the LDS key array (two
 // stations per broadcast ds_read_b128): scaled keys dot2(32 p, m) + c, else (dot2(p, m) << 10) + c
@@ -1978,7 +2017,8 @@ static int match_scn(const mev_ctx* ctx) {
 // LDS per workgroup of the fused LDSA kernel beyond the tables: each wave's n_b histogram and
 // episode draw table.
 static size_t lds_per_wave(const KParams& kp) {
-  return sizeof(int) * (size_t)kp.envs_per_wave * (8 + (size_t)kp.B * kp.hist_lds + kp.tab_m);
+  return sizeof(int) * (size_t)kp.envs_per_wave *
+         (8 + (size_t)kp.B * kp.hist_lds + kp.tab_m + kp.lbs);
 }
 // STG staging per wave and row (reward float32 + done byte per env), and for `rows` rows of
 // a workgroup of nw waves (only the compile-time-U kernels stage: U = 5, 15, 30)
@@ -2278,6 +2318,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.movement_reseed = params->movement_reseed;
   kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
   kp.hist_lds = params->num_ues <= 64 && kp.envs_per_wave * params->num_bs <= 1024;
+  kp.lbs = (params->bs_per_env && params->num_bs <= 16 && params->num_ues <= 64) ? 16 : 0;
   kp.Wd = (double)params->width;
   kp.Hd = (double)params->height;
   kp.vel = params->velocity;
