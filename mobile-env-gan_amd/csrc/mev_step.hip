@@ -370,7 +370,10 @@ constexpr int kWavesPerBlock = kPackedBlock / 64;
 constexpr int kLdsWaves = MEV_LDS_WAVES;
 // the two-read tables (LDSM 2: + a 2-byte rank per cell, ~141 KB for 200 x 200) take one
 // 16-wave workgroup per CU, the whole LDS
-constexpr int kLds2Waves = 16;
+#ifndef MEV_LDS2_WAVES
+#define MEV_LDS2_WAVES 16
+#endif
+constexpr int kLds2Waves = MEV_LDS2_WAVES;
 constexpr int kLds2BytesPerWG = 160 * 1024;
 __host__ __device__ constexpr int lds_waves(int ldsm) {
   return ldsm == 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
@@ -843,26 +846,28 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     const bool staged = FUSED && (SCN ? 0 : kp.lbs) != 0;  // (uniform)
     const int nb = staged ? nb_f : st.bs_count ? (valid ? st.bs_count[e] : 0) : KPS(B);
     const int2* bs = st.bs_xy + (size_t)e * KPS(B);
+    int d2s;
     if (staged) {
-      // the env's stations from its LDS slots (staged once per launch, 4 per ds_read_b128;
-      // slots past the env's count hold its last station again -- same d2, larger index: the
-      // original wins, as python's min keeps the first)
-      if (active && nb > 0) {
-        const v4u32* sv = reinterpret_cast<const v4u32*>(lbs + m.seg * 16);
+      // the env's station keys from its LDS slots (staged once per launch, two stations per
+      // ds_read_b128): one v_dot2 per station and a v_min3 per two, branch-free over 8 or 16
+      // slots (the never-winning padding keys fill the rest)
+      (void)nb;
+      const s16x2 p2 = {(short)(pos.x << 1), (short)(pos.y << 1)};
+      const v4u32* sv = reinterpret_cast<const v4u32*>(lbs + m.seg * 32);
+      auto scan = [&](auto npair) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q * 4 >= KPS(B)) break;
+        for (int q = 0; q < decltype(npair)::value; ++q) {
           const v4u32 w = sv[q];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int j = q * 4 + i;
-            if (j >= KPS(B)) break;
-            const s16x2 d = pu - as_s16x2(w[i]);  // coordinates < 1024
-            const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
-            best = min(best, (d2 << kKeyBits) | (unsigned)j);
-          }
+          const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p2, as_s16x2(w.x), (int)w.y, false);
+          const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p2, as_s16x2(w.z), (int)w.w, false);
+          best = min(best, min(k0, k1));
         }
-      }
+      };
+      if (KPS(B) <= 8) scan(std::integral_constant<int, 4>());
+      else scan(std::integral_constant<int, 8>());
+      if (!active) best = UINT_MAX;
+      d2s = (int)(best >> 4) - (1 << 21) + __mul24(pos.x, pos.x) + __mul24(pos.y, pos.y);
+      if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & 15u);
     } else if (active && nb > 0) {
       const int nb8 = (KPS(B) + 7) & ~7;  // wave-uniform trip count; j clamped to the last
       for (int b0 = 0; b0 < nb8; b0 += 8) {
@@ -876,8 +881,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         }
       }
     }
-    const int d2s = (int)(best >> kKeyBits);
-    if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & ((1u << kKeyBits) - 1));
+    if (!staged) {
+      d2s = (int)(best >> kKeyBits);
+      if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & ((1u << kKeyBits) - 1));
+    }
     // full-rate entry of the serving pair (index clamped: lanes without a server read a
     // valid entry)
     full = tb.rate_full[max(0, min(d2s, kp.d2max))];
@@ -1206,9 +1213,12 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   const LaneMap m = lane_map<PC>(lane, P);
   // per wave: stream slots [G][2] u128 {state, inc}, the n_b histogram, the group's episode
   // draw tables (x, y pairs) in LDS for the whole launch (lds_per_wave)
+  // (per-env station keys right after the stream slots: 16-byte aligned for ds_read_b128)
+  const int LB = SCN ? 0 : kp.lbs;  // ints per env of the staged station keys
   u128* lpcg = reinterpret_cast<u128*>(lds_hist) + wv * G * 2;
-  int* hist = lds_hist + NW * G * 8 + wv * G * KPS(B) * KPS(hist_lds);
-  int* ltab = lds_hist + NW * G * 8 + NW * G * KPS(B) * KPS(hist_lds) + wv * G * KPS(tab_m);
+  int* lbs = lds_hist + NW * G * 8 + wv * G * LB;
+  int* hist = lds_hist + NW * G * (8 + LB) + wv * G * KPS(B) * KPS(hist_lds);
+  int* ltab = lds_hist + NW * G * (8 + LB + KPS(B) * KPS(hist_lds)) + wv * G * KPS(tab_m);
   // STG (LDS-table trajectory launches, lean outputs): the per-env rows (reward float32, done
   // byte) of the workgroup's NW * G consecutive envs are staged in LDS for stage_rows steps and
   // then written by the whole workgroup as contiguous row pieces (128 B of reward per row for
@@ -1217,9 +1227,8 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   // uniform over the workgroup (its barriers): waves past the last group only take part in them.
   constexpr bool STG = LDSM == 2 && LEAN && UC != 0;
   constexpr int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
-  int* lbs = lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m)) + wv * G * (SCN ? 0 : kp.lbs);
-  float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + KPS(B) * KPS(hist_lds) + KPS(tab_m) +
-                                                              (SCN ? 0 : kp.lbs)));
+  float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + LB + KPS(B) * KPS(hist_lds) +
+                                                              KPS(tab_m)));
   uint8_t* sdone = reinterpret_cast<uint8_t*>(srew + (STG ? stage_rows * NWG : 0));
   const int gstride = LDSA ? (int)gridDim.x * NW : ngroups;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -1243,17 +1252,26 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
         if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
     }
     GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
-    // per-env layouts: the env's station count and its stations in the wave's LDS slots
+    // per-env layouts: the env's station keys in the wave's LDS slots, 16 per env, as
+    // {m = -16 q (int16x2), c = ((|q|^2 + 2^21) << 4) | j}, so that the key of station j for
+    // a UE at p is ONE dot product: dot2(2 p, m) + c = ((|p - q|^2 - |p|^2 + 2^21) << 4) | j
+    // (coordinates < 1024: |2 p|, |16 q| < 2^15, and the key < 2^32); slots past the env's
+    // count hold {0, UINT_MAX}, a key that never wins
     int nb_f = 0;
-    if (PER_ENV_BS && (SCN ? 0 : kp.lbs)) {
+    if (PER_ENV_BS && LB) {
       const int ec = min(e, kp.E - 1);
-      nb_f = st.bs_count ? st.bs_count[ec] : KPS(B);
+      nb_f = env_ok ? (st.bs_count ? st.bs_count[ec] : KPS(B)) : 0;
       if (m.seg < G)  // (lanes past the last segment hold no env)
         for (int k = m.u; k < 16; k += P) {
-          const int2 q = st.bs_xy[(size_t)ec * KPS(B) + max(0, min(k, nb_f - 1))];
-          lbs[m.seg * 16 + k] = (int)(((unsigned)q.x & 0xffffu) | ((unsigned)q.y << 16));
+          int2 kv = make_int2(0, -1);
+          if (k < nb_f) {
+            const int2 q = st.bs_xy[(size_t)ec * KPS(B) + k];
+            const s16x2 m2 = {(short)(-16 * q.x), (short)(-16 * q.y)};
+            kv = make_int2(__builtin_bit_cast(int, m2),
+                           (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << 4) | (unsigned)k));
+          }
+          *reinterpret_cast<int2*>(lbs + m.seg * 32 + 2 * k) = kv;
         }
-      if (!env_ok) nb_f = 0;
     }
     const bool leader = ROWS ? m.u == P - 1 : m.u == 0;
     ulonglong2 pa = make_ulonglong2(0, 0), pb = pa;
@@ -2318,7 +2336,8 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.movement_reseed = params->movement_reseed;
   kp.envs_per_wave = params->num_ues <= 64 ? 64 / params->num_ues : 1;
   kp.hist_lds = params->num_ues <= 64 && kp.envs_per_wave * params->num_bs <= 1024;
-  kp.lbs = (params->bs_per_env && params->num_bs <= 16 && params->num_ues <= 64) ? 16 : 0;
+  // 16 station key slots {m, c} per env (2 ints each; see k_steps_packed's staging)
+  kp.lbs = (params->bs_per_env && params->num_bs <= 16 && params->num_ues <= 64) ? 32 : 0;
   kp.Wd = (double)params->width;
   kp.Hd = (double)params->height;
   kp.vel = params->velocity;
