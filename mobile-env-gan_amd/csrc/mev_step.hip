@@ -79,7 +79,8 @@ struct KParams {
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
   int lds_assoc;      // bytes of the blob (multiple of 16)
-  int lds_mode;       // 1: station map + rank index; 2: + per-cell rank map (see packed_group)
+  int lds_mode;       // 1: station map + rank index; 2: + per-cell rank map; 3: per-cell
+                      // {station, rank in the layout's own d2 set} (see KTables::lds_blob)
   int lds_st_off, lds_rank_off, lds_rate_off, lds_r100_off, lds_r16_off;  // byte offsets
   double Wd, Hd, vel, lower, upper, w1, w2, log_w3, util_sat;
   double qoe_low;
@@ -148,6 +149,12 @@ struct KTables {
   //   [lds_rate_off, ...)      rate_full[d] for d in S, in increasing d (rank of d in S)
   // so full = rate[rank(d2)] with d2 to the serving station: the same float64 values as
   // `assoc`, from four LDS reads instead of one 16-byte gather from L2 per UE and step.
+  // Mode 2 adds a per-cell u16 rank at lds_r16_off (two parallel reads, then the rate). Mode 3
+  // (the default; cells <= 65536): ONE u16 per cell at offset 0, (station << 12) | k with k the
+  // rank of the cell's d2 in D, the set of squared distances that occur between a cell and its
+  // serving station in this layout (|D| is ~900 for mobile-large, ~3,300 for mobile-small);
+  // 0xF000 = no station in reach, 0xFFFF = k beyond 4094 (such cells take the L2 map);
+  // [lds_r100_off, +576) 100 / n; [lds_rate_off, +32 KB) rate_full[d] for d in D, in increasing d.
   const int4* lds_blob;
   // heterogeneous entities (KParams::het): per station class cb / UE class cu
   const uint8_t* bs_cls;    // [B] class of station j
@@ -221,7 +228,7 @@ __device__ __forceinline__ u128 pcg_draw_pair_next(u128 s, u128 inc, double w, d
 }
 
 // Registered scenarios with default parameters (medium, large; 200 x 200 map, default channel,
-// NoDeparture, draw table 3U + 8, the per-cell-rank LDS tables): their rollout launches run
+// NoDeparture, draw table 3U + 8, the LDS tables of mode 3): their rollout launches run
 // an instance with these values as constants (SCN > 0; fewer kernel arguments held in
 // SGPRs: -3 % time per step), chosen on the host only when every value matches the context's.
 struct ScnConst {
@@ -235,10 +242,12 @@ struct ScnConst {
 __host__ __device__ constexpr ScnConst scn_const(int scn) {
 #define MEV_SCN_F32 2, 1, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
                     0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u
-  return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 20000, 100000, 100576, 141392,
+  // (LDS tables of mode 3 for 200 x 200: cell entries [0, 80000), 100/n at 80000, rates at
+  // 80576, 113344 bytes in all)
+  return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 0, 80000, 80576, 113344,
                              MEV_SCN_F32}
-       : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 20000, 100000, 100576,
-                             141392, MEV_SCN_F32}
+       : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 0, 80000, 80576, 113344,
+                             MEV_SCN_F32}
                   : ScnConst{};
 }
 #define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
@@ -376,7 +385,7 @@ constexpr int kLdsWaves = MEV_LDS_WAVES;
 constexpr int kLds2Waves = MEV_LDS2_WAVES;
 constexpr int kLds2BytesPerWG = 160 * 1024;
 __host__ __device__ constexpr int lds_waves(int ldsm) {
-  return ldsm == 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
+  return ldsm >= 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
 }
 constexpr int kLdsBytesPerWG = 80 * 1024;
 
@@ -898,10 +907,27 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       // positions stay on the map (uniform draws in [0, W) x [0, H), moves toward waypoints
       // there), so the cell index is only bounded, not clamped per coordinate
       const uint32_t cell = min((uint32_t)(__mul24(pos.y, KPS(W)) + pos.x), (uint32_t)(KPS(W) * KPS(H) - 1));
-      const uint32_t nib =
+      const uint32_t nib = LDSM == 3 ? 0u :
           ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell >> 1)) >> ((cell & 1u) << 2)) &
           15u;
-      if (LDSM == 2) {  // rank of the cell's d2 from the per-cell map, read beside the nibble
+      if (LDSM == 3) {
+        // one u16 per cell: {station, rank of d2 in the layout's set D}, then the rate (read
+        // for every lane: entries without a station index a valid slot)
+        const uint32_t ent = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell);
+        const double fr = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent & 4095u));
+        if (active && ent < 0xF000u) {
+          srv = (int)(ent >> 12);
+          full = fr;
+        }
+        if (bal(ent == 0xFFFFu) & act_w) {  // cells whose rank lies beyond the table: L2 map
+          if (active && ent == 0xFFFFu) {
+            const int4 r = at(const_cast<int4*>(tb.assoc), 16u * cell);
+            srv = r.x;
+            full = __hiloint2double(r.w, r.z);
+          }
+          wait_vmem();  // in the load's own block (see the fallback draws)
+        }
+      } else if (LDSM == 2) {  // rank of the cell's d2 from the per-cell map, read beside the nibble
         const uint32_t k = *reinterpret_cast<const uint16_t*>(lblob + KPS(lds_r16_off) + 2u * cell);
         if (active && nib != 15u) {
           srv = (int)nib;
@@ -1225,7 +1251,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   // mobile-large) -- instead of every wavefront writing 2 x 4 B and 2 x 1 B pieces of each row
   // (measured: those partial-line writes cost 1.5 of 13.5 us per step). The group loop is then
   // uniform over the workgroup (its barriers): waves past the last group only take part in them.
-  constexpr bool STG = LDSM == 2 && LEAN && UC != 0;
+  constexpr bool STG = LDSM >= 2 && LEAN && UC != 0;
   constexpr int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
   float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + LB + KPS(B) * KPS(hist_lds) +
                                                               KPS(tab_m)));
@@ -1855,6 +1881,65 @@ __global__ void k_lds_map(const int2* __restrict__ bs, int B, int cells,
   blob[i] = (uint8_t)((sv[0] < 0 ? 15 : sv[0]) | ((sv[1] < 0 ? 15 : sv[1]) << 4));
 }
 
+// Mode-3 tables (KTables::lds_blob), built from the association map on the device in three
+// launches: the set D of squared distances between a cell and its serving station (bit d of
+// word d / 32), its rank index {bits, prefix}, then the u16 cell entries and rate_full over D.
+__global__ void k_d2_mark(const int4* __restrict__ map, int cells, uint2* __restrict__ words) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cells) return;
+  const int4 r = map[i];
+  if (r.x >= 0) atomicOr(&words[(uint32_t)r.y >> 5].x, 1u << ((uint32_t)r.y & 31u));
+}
+
+// Exclusive prefix counts of the words' bits (one workgroup of 1024 threads, each a contiguous
+// run of words).
+__global__ __launch_bounds__(1024) void k_d2_prefix(uint2* __restrict__ words, int nwords) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (nwords + 1023) / 1024;
+  const int w0 = min(t * per, nwords), w1 = min(w0 + per, nwords);
+  uint32_t c = 0;
+  for (int w = w0; w < w1; ++w) c += (uint32_t)__popc(words[w].x);
+  part[t] = c;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - c;
+  for (int w = w0; w < w1; ++w) {
+    words[w].y = run;
+    run += (uint32_t)__popc(words[w].x);
+  }
+}
+
+constexpr uint32_t kLds3Rates = 4096;  // rate slots of a mode-3 blob (ranks 0..4094 used)
+
+__global__ void k_lds_map3(const int4* __restrict__ map, int cells, const uint2* __restrict__ words,
+                           int d2max, const double* __restrict__ rate_full,
+                           uint8_t* __restrict__ blob, int rate_off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  auto rank = [&](uint32_t d2) {
+    const uint2 w = words[d2 >> 5];
+    return w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
+  };
+  if (i < cells) {
+    const int4 r = map[i];
+    uint32_t ent = 0xF000u;  // no station in reach
+    if (r.x >= 0) {
+      const uint32_t k = rank((uint32_t)r.y);
+      ent = k < kLds3Rates - 1 ? ((uint32_t)r.x << 12) | k : 0xFFFFu;
+    }
+    reinterpret_cast<uint16_t*>(blob)[i] = (uint16_t)ent;
+  }
+  if (i <= d2max && ((words[(uint32_t)i >> 5].x >> (i & 31)) & 1u)) {
+    const uint32_t k = rank((uint32_t)i);
+    if (k < kLds3Rates - 1) reinterpret_cast<double*>(blob + rate_off)[k] = rate_full[i];
+  }
+}
+
 // Episode draw table of the envs with mask[e] (all if NULL): pair k of env e = draws 2k and
 // 2k + 1 of the stream re-seeded to state0 (what every episode of the env draws, in order),
 // and the stream state after them. One thread per (env, pair).
@@ -1912,6 +1997,8 @@ struct mev_ctx {
   int4* assoc;    // [H][W] association map of the shared layout (mev_update_stations)
   int4* blob;     // its compact LDS form (KTables::lds_blob; null when it does not fit)
   uint2* rankw;   // {bits, prefix} rank index of the sums of two squares <= d2max (global)
+  uint2* dwords;  // mode 3: {bits, prefix} of the layout's serving-d2 set D (mev_update_stations)
+  int nwords;     // words of rankw / dwords (d2max / 32 + 1)
   int lds_wgs;    // resident workgroups of the LDSA fused kernel (CUs x per CU)
   int stage_rows; // mode 2: rows of per-env outputs the lean fused kernel stages in LDS (STG)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
@@ -2019,7 +2106,7 @@ static int match_scn(const mev_ctx* ctx) {
     if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
         kp.hist_lds == c.hist_lds && kp.t_end == c.t_end && kp.arr_start == c.arr_start &&
         kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
-        kp.lds_mode == 2 && kp.lds_r16_off == c.lds_r16_off &&
+        kp.lds_mode == 3 &&
         kp.lds_r100_off == c.lds_r100_off && kp.lds_rate_off == c.lds_rate_off &&
         kp.lds_assoc == c.lds_assoc && kp.d2snap == c.d2snap && kp.axis_exact == c.axis_exact &&
         fbits(kp.vel_f) == c.vel_f && fbits(kp.move_lim) == c.move_lim &&
@@ -2056,8 +2143,8 @@ static int build_lds_tables(mev_ctx* c) {
   KParams& kp = c->kp;
   kp.lds_assoc = 0;
   kp.lds_mode = 0;
-  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 force a mode
-  const int want = sw ? atoi(sw) : 2;
+  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 / 3 force a mode
+  const int want = sw ? atoi(sw) : 3;
   if (want == 0 || c->p.bs_per_env || kp.B > 15 || kp.U > 64 || c->d2max < 0) return MEV_OK;
   const int cells = kp.W * kp.H;
   const int d2max = c->d2max;
@@ -2078,13 +2165,24 @@ static int build_lds_tables(mev_ctx* c) {
   // the rank index in global memory too: k_lds_map derives the per-cell ranks (mode 2)
   if (hipMalloc(&c->rankw, 8 * nwords) != hipSuccess) return MEV_ENOMEM;
   MEV_HIP(hipMemcpy(c->rankw, rank.data(), 8 * nwords, hipMemcpyHostToDevice));
+  c->nwords = (int)nwords;
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t nib_bytes = up16(((size_t)cells + 1) / 2);
   // mode 2: [cell nibbles][cell ranks u16][100/n][rates]; mode 1: [cell nibbles][stations]
   // [rank index][100/n][rates]
   size_t st_off = 0, rank_off = 0, r16_off = 0, r100_off, rate_off, total;
   int mode = 0;
-  if (want >= 2 && count < 65536) {
+  if (want >= 3 && cells <= 65536) {  // [cell entries u16][100/n][rates over D]
+    r100_off = up16(2 * (size_t)cells);
+    rate_off = r100_off + 8 * 72;
+    total = up16(rate_off + 8 * (size_t)kLds3Rates);
+    if (total + kLds2Waves * (lds_per_wave(kp) + stage_bytes_per_row(kp)) + 4 <=
+        (size_t)kLds2BytesPerWG) {
+      if (hipMalloc(&c->dwords, 8 * nwords) != hipSuccess) return MEV_ENOMEM;
+      mode = 3;
+    }
+  }
+  if (!mode && want >= 2 && count < 65536) {
     r16_off = nib_bytes;
     r100_off = up16(r16_off + 2 * (size_t)cells);
     rate_off = r100_off + 8 * 72;
@@ -2106,16 +2204,21 @@ static int build_lds_tables(mev_ctx* c) {
   std::vector<double> full((size_t)d2max + 1);
   MEV_HIP(hipMemcpy(full.data(), c->rate_full, sizeof(double) * full.size(),
                     hipMemcpyDeviceToHost));
-  const size_t host_off = mode == 2 ? r100_off : st_off;  // the layout-independent part
+  const size_t host_off = mode >= 2 ? r100_off : st_off;  // the layout-independent part
   std::vector<char> host(total - host_off, 0);
   if (mode == 1) memcpy(host.data() + (rank_off - host_off), rank.data(), 8 * nwords);
   double* r100 = reinterpret_cast<double*>(host.data() + (r100_off - host_off));
   for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
   double* rates = reinterpret_cast<double*>(host.data() + (rate_off - host_off));
-  for (int d = 0, k = 0; d <= d2max; ++d)
-    if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) rates[k++] = full[(size_t)d];
+  if (mode <= 2)
+    for (int d = 0, k = 0; d <= d2max; ++d)
+      if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) rates[k++] = full[(size_t)d];
   if (hipMalloc(&c->blob, total) != hipSuccess) return MEV_ENOMEM;
-  MEV_HIP(hipMemset(c->blob, 0xff, nib_bytes));  // no station anywhere until a layout is set
+  if (mode == 3) {  // no station anywhere until a layout is set (0xF000), rates zero
+    MEV_HIP(hipMemset(c->blob, 0, total));
+    MEV_HIP(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(c->blob), 0xF000, (size_t)cells));
+  }
+  if (mode <= 2) MEV_HIP(hipMemset(c->blob, 0xff, nib_bytes));  // no station anywhere until a layout is set
   if (mode == 2) MEV_HIP(hipMemset(reinterpret_cast<char*>(c->blob) + r16_off, 0, r100_off - r16_off));
   MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + host_off, host.data(), host.size(),
                     hipMemcpyHostToDevice));
@@ -2131,7 +2234,7 @@ static int build_lds_tables(mev_ctx* c) {
   MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const int nw = lds_waves(mode);
   const size_t shmem = total + nw * lds_per_wave(kp);
-  c->stage_rows = mode == 2 ? (int)(((size_t)kLds2BytesPerWG - shmem - 4) /
+  c->stage_rows = mode >= 2 ? (int)(((size_t)kLds2BytesPerWG - shmem - 4) /
                                     (nw * stage_bytes_per_row(kp)))
                             : 0;
   if (const char* sr = getenv("MEV_STAGE_ROWS"))  // test switch: shorter staging windows
@@ -2512,6 +2615,7 @@ void mev_destroy(mev_ctx* c) {
   if (c->assoc) (void)hipFree(c->assoc);
   if (c->blob) (void)hipFree(c->blob);
   if (c->rankw) (void)hipFree(c->rankw);
+  if (c->dwords) (void)hipFree(c->dwords);
   if (c->tab_xy) (void)hipFree(c->tab_xy);
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
@@ -2535,7 +2639,7 @@ const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullp
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
   const bool lean_ok = !c->kp.util_direct;
-  return (c->kp.lds_assoc > 0 && c->kp.lds_mode == 2 && !c->p.bs_per_env && lean_ok)
+  return (c->kp.lds_assoc > 0 && c->kp.lds_mode == 3 && !c->p.bs_per_env && lean_ok)
              ? match_scn(c) : 0;
 }
 
@@ -2610,6 +2714,7 @@ static StepsKernel steps_kernel_u(int U) {
 
 static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U) {
   if (per_env) return lean ? steps_kernel_u<true, true, 0>(U) : steps_kernel_u<true, false, 0>(U);
+  if (ldsm == 3) return lean ? steps_kernel_u<false, true, 3>(U) : steps_kernel_u<false, false, 3>(U);
   if (ldsm == 2) return lean ? steps_kernel_u<false, true, 2>(U) : steps_kernel_u<false, false, 2>(U);
   if (ldsm == 1) return lean ? steps_kernel_u<false, true, 1>(U) : steps_kernel_u<false, false, 1>(U);
   return lean ? steps_kernel_u<false, true, 0>(U) : steps_kernel_u<false, false, 0>(U);
@@ -2635,16 +2740,16 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const bool ldsa = kp.lds_assoc > 0 && !c->p.bs_per_env && traj;
     const int ldsm = ldsa ? kp.lds_mode : 0;
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
-    if (ldsm == 2 && lean) {  // a registered scenario's constants (scn_const)
+    if (ldsm == 3 && lean) {  // a registered scenario's constants (scn_const)
       const int scn = match_scn(c);
-      if (scn == 1) kf = k_steps_packed<false, true, 15, 2, 1>;
-      if (scn == 2) kf = k_steps_packed<false, true, 30, 2, 2>;
+      if (scn == 1) kf = k_steps_packed<false, true, 15, 3, 1>;
+      if (scn == 2) kf = k_steps_packed<false, true, 30, 3, 2>;
     }
     const int nw = lds_waves(ldsm);
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
     size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
-    const bool stg = ldsm == 2 && lean && stages(kp);  // k_steps_packed STG
+    const bool stg = ldsm >= 2 && lean && stages(kp);  // k_steps_packed STG
     const int srows = stg ? std::min(c->stage_rows, nsteps) : 1;
     kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
          stream>>>(kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
@@ -2737,7 +2842,18 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                      reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
                      c->p.height, c->d2max, c->rate_full, c->assoc);
   MEV_HIP(hipGetLastError());
-  if (c->blob) {
+  if (c->blob && c->kp.lds_mode == 3) {
+    MEV_HIP(hipMemsetAsync(c->dwords, 0, 8 * (size_t)c->nwords, (hipStream_t)stream));
+    hipLaunchKernelGGL(k_d2_mark, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       c->assoc, cells, c->dwords);
+    hipLaunchKernelGGL(k_d2_prefix, dim3(1), dim3(1024), 0, (hipStream_t)stream, c->dwords,
+                       c->nwords);
+    const int n = std::max(cells, c->d2max + 1);
+    hipLaunchKernelGGL(k_lds_map3, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       c->assoc, cells, c->dwords, c->d2max, c->rate_full,
+                       reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_rate_off);
+    MEV_HIP(hipGetLastError());
+  } else if (c->blob) {
     const int bytes = (cells + 1) / 2;
     hipLaunchKernelGGL(k_lds_map, dim3((bytes + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, cells, c->assoc,
