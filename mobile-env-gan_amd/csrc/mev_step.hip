@@ -1192,12 +1192,11 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
 // STG: the workgroup writes its staged per-env rows [row0, row0 + nr) x [e0, e0 + NWG) (reward
 // float32, done byte) with consecutive threads on consecutive envs, between two barriers (the
 // slots are complete before, and free for the next steps after).
-template <int NT, int NWG>
 __device__ __forceinline__ void flush_staged(const KOut& out, const float* srew,
                                              const uint8_t* sdone, int E, int e0, int row0,
-                                             int nr) {
+                                             int nr, int NWG) {
   __syncthreads();
-  for (int q = threadIdx.x; q < nr * NWG; q += NT) {
+  for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     const int r = q / NWG, j = q - r * NWG;
     if (e0 + j < E) {
       const size_t ro = (size_t)(row0 + r) * (size_t)E;
@@ -1215,7 +1214,9 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     int stage_rows) {
   extern __shared__ int lds_all[];
   constexpr bool LDSA = LDSM != 0;
-  constexpr int NW = lds_waves(LDSM);  // waves per workgroup
+  // waves per workgroup: up to lds_waves(LDSM) (the launch bounds); LDSA launches with few
+  // groups take fewer, so that the workgroups spread over every CU
+  const int NW = (int)(blockDim.x >> 6);
   int* lds_hist = lds_all;
   const char* lblob = nullptr;
   if (LDSA) {
@@ -1252,7 +1253,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   // (measured: those partial-line writes cost 1.5 of 13.5 us per step). The group loop is then
   // uniform over the workgroup (its barriers): waves past the last group only take part in them.
   constexpr bool STG = LDSM >= 2 && LEAN && UC != 0;
-  constexpr int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
+  const int NWG = NW * (PC ? 64 / (PC ? PC : 1) : 1);  // envs per workgroup tile (STG)
   float* srew = reinterpret_cast<float*>(lds_hist + NW * G * (8 + LB + KPS(B) * KPS(hist_lds) +
                                                               KPS(tab_m)));
   uint8_t* sdone = reinterpret_cast<uint8_t*>(srew + (STG ? stage_rows * NWG : 0));
@@ -1262,8 +1263,8 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     const int g = gb + wvu;
     if (STG && g >= ngroups) {  // no group for this wave: its part of the flushes only
       for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-        flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i0 : 0,
-                                   min(stage_rows, nsteps - i0));
+        flush_staged(out, srew, sdone, kp.E, gb * G, traj ? i0 : 0, min(stage_rows, nsteps - i0),
+                     NWG);
       continue;
     }
     const int e = g * G + m.seg;
@@ -1329,7 +1330,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, lblob, lpcg,
           srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w, lbs, nb_f);
       if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
-        flush_staged<NW * 64, NWG>(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1);
+        flush_staged(out, srew, sdone, kp.E, gb * G, traj ? i - sr : 0, sr + 1, NWG);
     }
     if (!LDSA)  // the last step's deferred outputs
       flush_pending<LEAN>(out, pend, (uint32_t)kp.E, (uint32_t)(kp.E * U),
@@ -1357,6 +1358,384 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
         const u128 sl = lpcg[2 * m.seg];
         const ulonglong2 sf = a.s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
         at(pcg2, 48u * (uint32_t)e) = sf;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Two env groups per wavefront: k_steps_lds2 (trajectory rollouts, mode-3 LDS tables)
+// ------------------------------------------------------------------------------------
+// The LDS tables (mode 3, 113 KB for 200 x 200) leave room for one 16-wave workgroup per CU,
+// i.e. 4 waves per SIMD; a rollout step at that occupancy waits on its own dependency chains
+// (LDS reads, ballots, the DPP sums) much of the time (measured: 2 waves per SIMD 16.6 vs 4
+// waves 11.6 us per step). Here each wavefront advances TWO env groups (contexts r = 0, 1) in
+// one instruction stream: the common path of a step is branch-free (movement, association,
+// n_b, share, utility, sums and stores computed for every lane and selected), so the two
+// contexts' instructions sit in the same basic blocks and the scheduler interleaves them. The
+// rare paths (fallback draws past the draw table, the exact float64 movement, share ties, far
+// cells, episode resets) are wave-uniform branches per context. Same results as packed_group
+// bit for bit (tests). Shapes: U = 15 / 30 at compile time (aligned segments), lean outputs,
+// a draw table (tab_m > 0), staged per-env rows.
+struct Ctx2 {
+  int t, drawn;
+  bool s_ok, moved;
+  int2 pos, wp;
+};
+
+template <int UC, int SCN, int R>
+__device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
+                                          const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
+                                          const int (&e)[R], const bool (&env_ok)[R],
+                                          const uint64_t (&envok_w)[R],
+                                          const uint64_t (&valid_w)[R], int row,
+                                          const char* __restrict__ lblob, u128* __restrict__ lpcg,
+                                          int* __restrict__ hist, const int* __restrict__ ltab,
+                                          int* __restrict__ srow, uint8_t* __restrict__ drow) {
+  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  const int M = KPS(tab_m), B = KPS(B), HB = B + 1;
+  const int u = m.u;
+  const bool lead_lane = u == PC - 1;
+  bool valid[R], active[R], need[R], do_reset[R], reset_env[R];
+  int tot[R], rank[R];
+  uint64_t act_w[R], mneed_w[R];
+  // ---- A: lazy auto-reset, ballots (base.py:288-291) ----------------------------------------
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int er = r * G + m.seg;  // the env's slot among the wave's R * G
+    valid[r] = env_ok[r] && u < U;
+    reset_env[r] = env_ok[r] && c[r].t >= KPS(t_end);
+    do_reset[r] = reset_env[r] && valid[r];
+    if (bal(c[r].t >= KPS(t_end)) & envok_w[r]) {  // initial positions = the episode's first U
+      if (reset_env[r]) {                          // pairs of the draw table
+        c[r].t = 0;
+        c[r].drawn = U;
+      }
+      if (do_reset[r]) {
+        const int p = ltab[er * M + u];
+        c[r].pos = make_int2((int)(short)p, p >> 16);
+        c[r].wp = make_int2(-1, -1);
+      }
+    }
+    const int t = c[r].t;
+    const bool on = t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0);
+    active[r] = valid[r] && on;
+    act_w[r] = bal(on) & valid_w[r];
+    need[r] = active[r] && c[r].wp.x < 0;
+    mneed_w[r] = bal(c[r].wp.x < 0) & act_w[r];
+    const uint32_t f = seg_field<PC>(mneed_w[r], m);
+    tot[r] = __popc(f);
+    rank[r] = __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)u));
+  }
+  // ---- B: waypoint draws in ue_id order (movement.py:44-47) -----------------------------------
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int er = r * G + m.seg;
+    u128* const slot = lpcg + 2 * er;
+    bool fell_back = false;
+    u128 s_fin = 0;
+    if (mneed_w[r]) {
+      const int k = c[r].drawn + rank[r];
+      if ((bal(k >= M) & mneed_w[r]) == 0) {  // every pair precomputed (the common case)
+        if (need[r]) {
+          const int p = ltab[er * M + k];
+          c[r].wp = make_int2((int)(short)p, p >> 16);
+        }
+      } else {  // beyond the table: from the stream state (see packed_group)
+        fell_back = true;
+        const u128 inc = slot[1];
+        u128 s;
+        if (!c[r].s_ok && c[r].drawn > 0) {
+          s = at(const_cast<u128*>(tb.tab_st),
+                 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(min(c[r].drawn, M) - 1)));
+          wait_vmem();
+        } else {
+          s = slot[0];
+        }
+        if (reset_env[r]) {  // the state after this episode's U initial pairs
+          s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(U - 1)));
+          wait_vmem();
+        }
+        if ((bal(rank[r] != 0) & mneed_w[r]) == 0) {
+          if (need[r]) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
+        } else {
+          if (need[r])
+            s_fin = pcg_draw_pair(s, inc, 2 * rank[r], tb.jump, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
+        }
+        wait_vmem();
+      }
+    }
+    const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
+                         (do_reset[r] && tot[r] == 0 && u == U - 1);
+    if (fell_back && own_fin) slot[0] = s_fin;
+    if (fell_back && tot[r] > 0) c[r].s_ok = true;
+    else if (tot[r] > 0 || reset_env[r]) c[r].s_ok = false;
+    c[r].moved |= own_fin;
+    c[r].drawn += tot[r];
+  }
+  // ---- C: movement (movement.py:49-62), branch-free fast path --------------------------------
+  // (move_ue_p per lane: arrival snap; axis-parallel moves exactly in float32 when the velocity
+  // is a float32 value (scenario constants); the float32 step clear of a tie; else float64)
+  constexpr bool AXF = SCN != 0;  // scenario velocity 1.5: pos +- 1.5 exact in float32
+  int2 npos[R];
+  bool arrive[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int2 pos = c[r].pos, wp = c[r].wp;
+    const int dx = wp.x - pos.x, dy = wp.y - pos.y;
+    const int d2 = __mul24(dx, dx) + __mul24(dy, dy);
+    arrive[r] = d2 <= KPS(d2snap);
+    const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);
+    const float qx = (float)dx * sc, qy = (float)dy * sc;
+    const float rx = rintf(qx), ry = rintf(qy);
+    const bool axis = dx == 0 || dy == 0;
+    bool ok = fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < KPSF(move_lim);
+    int2 np = make_int2(pos.x + (int)rx, pos.y + (int)ry);
+    if (AXF) {
+      const float vs = KPSF(vel_f);
+      const int ax = (int)rintf((float)pos.x + (dx > 0 ? vs : -vs));
+      const int ay = (int)rintf((float)pos.y + (dy > 0 ? vs : -vs));
+      if (axis) np = dy == 0 ? make_int2(ax, pos.y) : make_int2(pos.x, ay);
+      ok = ok || axis;
+    }
+    const bool xneed = active[r] && !arrive[r] && !ok;
+    if (bal(xneed)) {  // rare: the exact float64 step (ties, non-float32 axis moves)
+      if (xneed) np = move_exact(pos, dx, dy, kp.vel);
+    }
+    npos[r] = arrive[r] ? wp : np;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (active[r]) {  // (selects)
+      c[r].pos = npos[r];
+      if (arrive[r]) c[r].wp = make_int2(-1, -1);
+    }
+  }
+  // ---- D: association (mode-3 LDS tables), n_b, share, utility ------------------------------
+  int srv[R];
+  double full[R];
+  uint32_t cell[R], ent[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    cell[r] = min((uint32_t)(__mul24(c[r].pos.y, KPS(W)) + c[r].pos.x),
+                  (uint32_t)(KPS(W) * KPS(H) - 1));
+    ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
+    full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent[r] & 4095u));
+    srv[r] = active[r] && ent[r] < 0xF000u ? (int)(ent[r] >> 12) : -1;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (bal(ent[r] == 0xFFFFu) & act_w[r]) {  // cells beyond the table's ranks: L2 map
+      if (active[r] && ent[r] == 0xFFFFu) {
+        const int4 q = at(const_cast<int4*>(tb.assoc), 16u * cell[r]);
+        srv[r] = q.x;
+        full[r] = __hiloint2double(q.w, q.z);
+      }
+      wait_vmem();
+    }
+  }
+  // per-env histograms in the wave's LDS (bin B: lanes without a station): zero, count, read
+  int* h[R];
+  int bin[R], n[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    h[r] = hist + (r * G + m.seg) * HB;
+    bin[r] = srv[r] >= 0 ? srv[r] : B;
+    h[r][min(u, B)] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    __hip_atomic_fetch_add(h[r] + bin[r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  __builtin_amdgcn_wave_barrier();
+  float cf[R];
+  bool tie[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    n[r] = min(h[r][bin[r]], 64);
+    const double r100 = *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n[r]);
+    // share_cents_r (ResourceFair share + numpy round(., 2)), the tie test in float32
+    const double cc = full[r] * r100;
+    const double rr = rint(cc);
+    const float d = (float)(cc - rr);
+    const float rf = (float)rr;
+    tie[r] = srv[r] >= 0 && !(0.5f - fabsf(d) > __builtin_fmaf(rf, 0x1p-46f, 0x1p-25f));
+    cf[r] = srv[r] >= 0 ? rf : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (bal(tie[r])) {  // rare: within 2^-46 of a half cent -- the reference's two divisions
+      if (tie[r]) cf[r] = (float)rint((full[r] / (double)n[r]) * 100.0);
+    }
+  }
+  // ---- E: utility, reward sum, stores -------------------------------------------------------
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float rate_f = cf[r] * 0.01f;
+    const float util = active[r] ? (float)utility_f32r<SCN>(cf[r], rate_f, kp) : 0.f;
+    const int isum = seg_isum_rows<PC>(active[r] ? (int)(util * 0x1p25f) : 0);
+    const int nact = __popc(seg_field<PC>(act_w[r], m));
+    Pending up;
+    up.srv = srv[r];
+    up.obs = make_float4((float)c[r].pos.x * KPSF(inv_w), (float)c[r].pos.y * KPSF(inv_h),
+                         rate_f, util);
+    up.ui = (uint32_t)(e[r] * U + u);
+    up.valid = valid[r];
+    up.lead = up.done = false;
+    up.e = 0;
+    up.reward = 0.f;
+    flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
+    // the env's staged row entry: the 2^-25 fixed-point utility sum and {nact, done}; the
+    // workgroup's flush forms the float32 reward from them. Lanes other than the env's last
+    // write into the histogram's spare bin instead (no branch).
+    const bool lead = env_ok[r] && lead_lane;
+    const int er = r * G + m.seg;
+    int* sw = lead ? srow + er : h[r] + B;
+    uint8_t* dw = lead ? drow + er : reinterpret_cast<uint8_t*>(h[r] + B);
+    *sw = isum;
+    *dw = (uint8_t)(nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0));
+    c[r].t += 1;
+  }
+}
+
+// The staged rows of k_steps_lds2: reward = (float)isum 2^-25 / nact (float32, as packed_group's
+// lean path), or the utility's lower bound without active UEs; done = bit 7.
+__device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
+                                              int E, int e0, int row0, int nr, float lower,
+                                              int NWG) {
+  __syncthreads();
+  for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
+    const int r = q / NWG, j = q - r * NWG;
+    if (e0 + j < E) {
+      const size_t ro = (size_t)(row0 + r) * (size_t)E;
+      const uint32_t o = (uint32_t)(e0 + j);
+      const uint32_t b = drow[q];
+      const int nact = (int)(b & 0x7fu);
+      at(out.reward + ro, 4u * o) =
+          nact > 0 ? (float)srow[q] * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
+      at(out.done + ro, o) = (uint8_t)(b >> 7);
+    }
+  }
+  __syncthreads();
+}
+
+// LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, histograms [R G][B + 1] int, draw
+// tables [R G][M] int
+__host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R) {
+  return sizeof(int) * (size_t)(R * G) * (8 + (size_t)(B + 1) + (size_t)M);
+}
+
+template <int UC, int SCN>
+__global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
+    KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
+    int stage_rows) {
+  constexpr int R = 2;
+  const int NW = (int)(blockDim.x >> 6);  // <= kLds2Waves
+  constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC;
+  const int NWG = NW * G * R;  // envs per workgroup tile
+  extern __shared__ int lds_all[];
+  {  // the tables: LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...
+    const int n16 = KPS(lds_assoc) >> 4;
+    const int ln = threadIdx.x & 63;
+    for (int q = (int)(threadIdx.x >> 6); q * 64 < n16; q += NW)
+      if (q * 64 + ln < n16) glds(tb.lds_blob + q * 64 + ln, reinterpret_cast<int4*>(lds_all) + q * 64);
+    wait_vmem();
+    __syncthreads();
+  }
+  const char* lblob = reinterpret_cast<const char*>(lds_all);
+  const int M = KPS(tab_m), B = KPS(B);
+  const int wv = threadIdx.x >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int lane = threadIdx.x & 63;
+  const LaneMap m = lane_map<PC>(lane, PC);
+  int* lw = lds_all + (KPS(lds_assoc) >> 2);
+  u128* lpcg = reinterpret_cast<u128*>(lw) + wv * R * G * 2;
+  int* hist = lw + NW * R * G * 8 + wv * R * G * (B + 1);
+  int* ltab = lw + NW * R * G * (8 + B + 1) + wv * R * G * M;
+  int* srow = lw + NW * R * G * (8 + B + 1 + M);
+  uint8_t* drow = reinterpret_cast<uint8_t*>(srow + stage_rows * NWG);
+  const int npairs = (ngroups + 1) / 2;
+  const int gstride = (int)gridDim.x * NW;
+  const float lower = (float)kp.lower;
+  for (int pb = block_slot(kp.xcd_remap) * NW; pb < npairs; pb += gstride) {
+    const int p = pb + wvu;
+    const int e0 = pb * G * R;  // the workgroup tile's first env
+    if (p >= npairs) {  // no pair for this wave: its part of the flushes only
+      for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
+        flush_staged2(out, srow, drow, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
+                      NWG);
+      continue;
+    }
+    Ctx2 c[R];
+    int e[R];
+    bool env_ok[R];
+    uint64_t envok_w[R], valid_w[R];
+    ulonglong2 pa[R], pbv[R];
+    const bool leader = m.u == PC - 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int g = 2 * p + r;
+      e[r] = g * G + m.seg;
+      env_ok[r] = (m.seg < G) && (e[r] < kp.E);
+      // the group's draw tables (LDS-DMA) and state, issued before one wait
+      const int nt = G * M;
+      const int lim = max(0, min(nt, (kp.E - g * G) * M));
+      const int* src = tb.tab_xy + (size_t)g * nt;
+      for (int q = 0; q * 64 < lim; ++q)
+        if (q * 64 + lane < lim) glds(src + q * 64 + lane, ltab + r * nt + q * 64);
+      const GroupIn a = load_group(kp, st, tb, e[r], min(m.u, U - 1), U, true);
+      c[r].t = a.t;
+      c[r].drawn = a.drawn;
+      c[r].s_ok = true;
+      c[r].moved = false;
+      c[r].pos = make_int2(a.s.x, a.s.y);
+      c[r].wp = make_int2(a.s.z, a.s.w);
+      pa[r] = pbv[r] = make_ulonglong2(0, 0);
+      if (env_ok[r] && leader) {
+        ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
+        pa[r] = at(pr, 48u * (uint32_t)e[r]);
+        pbv[r] = at(pr, 48u * (uint32_t)e[r] + 16u);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (env_ok[r] && leader) {
+        lpcg[2 * (r * G + m.seg)] = mk128(pa[r].x, pa[r].y);
+        lpcg[2 * (r * G + m.seg) + 1] = mk128(pbv[r].x, pbv[r].y);
+      }
+      envok_w[r] = bal(env_ok[r]);
+      valid_w[r] = bal(env_ok[r] && m.u < U);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int i = 0; i < nsteps; ++i) {
+      const int sr = i % stage_rows;
+      lds2_step<UC, SCN, R>(kp, st, out, tb, m, c, e, env_ok, envok_w, valid_w, traj ? i : 0, lblob,
+                            lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
+                            drow + sr * NWG + wvu * G * R);
+      if (sr == stage_rows - 1 || i == nsteps - 1)
+        flush_staged2(out, srow, drow, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG);
+    }
+    // the state after the last step (see k_steps_packed)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (env_ok[r] && m.u < U)
+        store_ue(&at(st.ue_state, 8u * (uint32_t)(e[r] * U + m.u)), c[r].pos, c[r].wp);
+      const bool mvd = seg_field<PC>(bal(c[r].moved), m) != 0u;
+      if (env_ok[r] && leader) {
+        at(st.t, 4u * (uint32_t)e[r]) = c[r].t;
+        at(tb.drawn, 4u * (uint32_t)e[r]) = c[r].drawn;
+        if (mvd) {
+          ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
+          const ulonglong2 tv = at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
+                                   16u * ((uint32_t)e[r] * (uint32_t)M +
+                                          (uint32_t)max(min(c[r].drawn, M) - 1, 0)));
+          const u128 sl = lpcg[2 * (r * G + m.seg)];
+          const ulonglong2 sf =
+              c[r].s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
+          at(pcg2, 48u * (uint32_t)e[r]) = sf;
+        }
       }
     }
   }
@@ -1882,24 +2261,31 @@ __global__ void k_lds_map(const int2* __restrict__ bs, int B, int cells,
 }
 
 // Mode-3 tables (KTables::lds_blob), built from the association map on the device in three
-// launches: the set D of squared distances between a cell and its serving station (bit d of
-// word d / 32), its rank index {bits, prefix}, then the u16 cell entries and rate_full over D.
-__global__ void k_d2_mark(const int4* __restrict__ map, int cells, uint2* __restrict__ words) {
+// launches: the set D of squared distances between a cell and its serving station (a flag
+// byte per d2: plain stores of the same value, no atomics), its rank index {bits, prefix} over
+// words of 32, then the u16 cell entries and rate_full over D.
+__global__ void k_d2_mark(const int4* __restrict__ map, int cells, uint8_t* __restrict__ flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cells) return;
   const int4 r = map[i];
-  if (r.x >= 0) atomicOr(&words[(uint32_t)r.y >> 5].x, 1u << ((uint32_t)r.y & 31u));
+  if (r.x >= 0) flag[r.y] = 1;
 }
 
-// Exclusive prefix counts of the words' bits (one workgroup of 1024 threads, each a contiguous
-// run of words).
-__global__ __launch_bounds__(1024) void k_d2_prefix(uint2* __restrict__ words, int nwords) {
+// The words' bits from the flags and their exclusive prefix counts (one workgroup of 1024
+// threads, each a contiguous run of words).
+__global__ __launch_bounds__(1024) void k_d2_prefix(const uint8_t* __restrict__ flag, int nflag,
+                                                    uint2* __restrict__ words, int nwords) {
   __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
   const int per = (nwords + 1023) / 1024;
   const int w0 = min(t * per, nwords), w1 = min(w0 + per, nwords);
   uint32_t c = 0;
-  for (int w = w0; w < w1; ++w) c += (uint32_t)__popc(words[w].x);
+  for (int w = w0; w < w1; ++w) {
+    uint32_t b = 0;
+    for (int k = 0; k < 32 && 32 * w + k < nflag; ++k) b |= (uint32_t)(flag[32 * w + k] != 0) << k;
+    words[w].x = b;
+    c += (uint32_t)__popc(b);
+  }
   part[t] = c;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
@@ -1998,8 +2384,12 @@ struct mev_ctx {
   int4* blob;     // its compact LDS form (KTables::lds_blob; null when it does not fit)
   uint2* rankw;   // {bits, prefix} rank index of the sums of two squares <= d2max (global)
   uint2* dwords;  // mode 3: {bits, prefix} of the layout's serving-d2 set D (mev_update_stations)
+  uint8_t* dflag; // mode 3: a flag byte per d2 in [0, d2max] (D before its rank index)
   int nwords;     // words of rankw / dwords (d2max / 32 + 1)
   int lds_wgs;    // resident workgroups of the LDSA fused kernel (CUs x per CU)
+  int lds2_wgs;   // ... of k_steps_lds2 (0: not used for this context)
+  int stage_rows2;
+  int stage_cap;  // MEV_STAGE_ROWS (test switch; 0: none)
   int stage_rows; // mode 2: rows of per-env outputs the lean fused kernel stages in LDS (STG)
   int parts;          // mev_step: 1 or 2 env halves (params.stream_split)
   int fuse_steps;     // mev_step(n > 1): one fused launch (params.fuse_steps)
@@ -2172,13 +2562,17 @@ static int build_lds_tables(mev_ctx* c) {
   // [rank index][100/n][rates]
   size_t st_off = 0, rank_off = 0, r16_off = 0, r100_off, rate_off, total;
   int mode = 0;
-  if (want >= 3 && cells <= 65536) {  // [cell entries u16][100/n][rates over D]
+  // mode 3 for aligned env segments (U -> 16 / 32 lanes); measured slower than mode 1 for
+  // mobile-small (U = 5: 162 vs 142 us per 40-step launch at 65,536 envs)
+  const bool aligned = pitch_of(kp.U) == 16 || pitch_of(kp.U) == 32;
+  if (want >= 3 && cells <= 65536 && (aligned || (sw && want == 3))) {  // [cell entries u16][100/n][rates over D]
     r100_off = up16(2 * (size_t)cells);
     rate_off = r100_off + 8 * 72;
     total = up16(rate_off + 8 * (size_t)kLds3Rates);
     if (total + kLds2Waves * (lds_per_wave(kp) + stage_bytes_per_row(kp)) + 4 <=
         (size_t)kLds2BytesPerWG) {
       if (hipMalloc(&c->dwords, 8 * nwords) != hipSuccess) return MEV_ENOMEM;
+      if (hipMalloc(&c->dflag, (size_t)d2max + 1) != hipSuccess) return MEV_ENOMEM;
       mode = 3;
     }
   }
@@ -2237,8 +2631,12 @@ static int build_lds_tables(mev_ctx* c) {
   c->stage_rows = mode >= 2 ? (int)(((size_t)kLds2BytesPerWG - shmem - 4) /
                                     (nw * stage_bytes_per_row(kp)))
                             : 0;
+  c->stage_cap = 0;
   if (const char* sr = getenv("MEV_STAGE_ROWS"))  // test switch: shorter staging windows
-    if (atoi(sr) > 0) c->stage_rows = std::min(c->stage_rows, atoi(sr));
+    if (atoi(sr) > 0) {
+      c->stage_cap = atoi(sr);
+      c->stage_rows = std::min(c->stage_rows, c->stage_cap);
+    }
   int per = 1 << 30;
   for (int lean = 0; lean < 2; ++lean) {
     int n = 0;
@@ -2248,6 +2646,23 @@ static int build_lds_tables(mev_ctx* c) {
     per = std::min(per, n);
   }
   c->lds_wgs = cus * per;
+  // two env groups per wavefront (k_steps_lds2): mode 3, U = 15 / 30, a draw table
+  c->lds2_wgs = 0;
+  const char* l2 = getenv("MEV_LDS2");  // dev / test switch: 0 = one group per wavefront
+  if (mode == 3 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !(l2 && atoi(l2) == 0)) {
+    const int G = kp.envs_per_wave;
+    const size_t sh2 = total + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2);
+    const size_t row2 = (size_t)kLds2Waves * G * 2 * 5;
+    if (sh2 + row2 + 4 <= (size_t)kLds2BytesPerWG) {
+      c->stage_rows2 = (int)(((size_t)kLds2BytesPerWG - sh2 - 4) / row2);
+      if (c->stage_cap > 0) c->stage_rows2 = std::min(c->stage_rows2, c->stage_cap);
+      int n2 = 0;
+      MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &n2, reinterpret_cast<const void*>(kp.U == 15 ? k_steps_lds2<15, 0> : k_steps_lds2<30, 0>),
+          64 * kLds2Waves, sh2 + (((size_t)c->stage_rows2 * row2 + 3) & ~(size_t)3)));
+      c->lds2_wgs = cus * n2;
+    }
+  }
   if (c->lds_wgs <= 0) {  // cannot be resident: the L2 gather path
     (void)hipFree(c->blob);
     c->blob = nullptr;
@@ -2616,6 +3031,7 @@ void mev_destroy(mev_ctx* c) {
   if (c->blob) (void)hipFree(c->blob);
   if (c->rankw) (void)hipFree(c->rankw);
   if (c->dwords) (void)hipFree(c->dwords);
+  if (c->dflag) (void)hipFree(c->dflag);
   if (c->tab_xy) (void)hipFree(c->tab_xy);
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
@@ -2739,18 +3155,40 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // stores stay in L2 and the tables' LDS cost occupancy, 4 vs 5 waves per SIMD)
     const bool ldsa = kp.lds_assoc > 0 && !c->p.bs_per_env && traj;
     const int ldsm = ldsa ? kp.lds_mode : 0;
+    // two env groups per wavefront when the batch fills every resident workgroup with them
+    const int pairs = (groups + 1) / 2;
+    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pairs >= c->lds2_wgs * kLds2Waves) {
+      const int scn = match_scn(c);
+      StepsKernel k2 = kp.U == 15 ? (scn == 1 ? k_steps_lds2<15, 1> : k_steps_lds2<15, 0>)
+                                  : (scn == 2 ? k_steps_lds2<30, 2> : k_steps_lds2<30, 0>);
+      const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
+      const int G = kp.envs_per_wave;
+      const int srows = std::min(c->stage_rows2, nsteps);
+      const size_t sh = (size_t)kp.lds_assoc + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2) +
+                        (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
+      k2<<<dim3(blocks), dim3(64 * kLds2Waves), sh, stream>>>(kp, ks, ko, tb, groups, nsteps, 1,
+                                                              srows);
+      MEV_HIP(hipGetLastError());
+      return MEV_OK;
+    }
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
     if (ldsm == 3 && lean) {  // a registered scenario's constants (scn_const)
       const int scn = match_scn(c);
       if (scn == 1) kf = k_steps_packed<false, true, 15, 3, 1>;
       if (scn == 2) kf = k_steps_packed<false, true, 30, 3, 2>;
     }
-    const int nw = lds_waves(ldsm);
+    int nw = lds_waves(ldsm);
+    if (ldsa)  // few groups: fewer waves per workgroup, the workgroups on every CU
+      nw = std::max(1, std::min(nw, (groups + c->lds_wgs - 1) / c->lds_wgs));
     int blocks = (groups + nw - 1) / nw;
     if (ldsa) blocks = std::min(blocks, c->lds_wgs);  // persistent: the resident workgroups
     size_t shmem_f = (ldsa ? (size_t)kp.lds_assoc : 0) + nw * lds_per_wave(kp);  // layout: k_steps_packed
     const bool stg = ldsm >= 2 && lean && stages(kp);  // k_steps_packed STG
-    const int srows = stg ? std::min(c->stage_rows, nsteps) : 1;
+    int srows = stg ? std::min(c->stage_rows, nsteps) : 1;
+    if (stg && nw < lds_waves(ldsm))  // (more rows fit beside fewer waves)
+      srows = std::min({nsteps, c->stage_cap > 0 ? c->stage_cap : nsteps,
+                        (int)(((size_t)kLds2BytesPerWG - shmem_f - 4) /
+                              ((size_t)nw * stage_bytes_per_row(kp)))});
     kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
          stream>>>(kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
     MEV_HIP(hipGetLastError());
@@ -2843,11 +3281,11 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                      c->p.height, c->d2max, c->rate_full, c->assoc);
   MEV_HIP(hipGetLastError());
   if (c->blob && c->kp.lds_mode == 3) {
-    MEV_HIP(hipMemsetAsync(c->dwords, 0, 8 * (size_t)c->nwords, (hipStream_t)stream));
+    MEV_HIP(hipMemsetAsync(c->dflag, 0, (size_t)c->d2max + 1, (hipStream_t)stream));
     hipLaunchKernelGGL(k_d2_mark, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       c->assoc, cells, c->dwords);
-    hipLaunchKernelGGL(k_d2_prefix, dim3(1), dim3(1024), 0, (hipStream_t)stream, c->dwords,
-                       c->nwords);
+                       c->assoc, cells, c->dflag);
+    hipLaunchKernelGGL(k_d2_prefix, dim3(1), dim3(1024), 0, (hipStream_t)stream, c->dflag,
+                       c->d2max + 1, c->dwords, c->nwords);
     const int n = std::max(cells, c->d2max + 1);
     hipLaunchKernelGGL(k_lds_map3, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        c->assoc, cells, c->dwords, c->d2max, c->rate_full,

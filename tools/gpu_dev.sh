@@ -16,7 +16,9 @@ fi
 IFS='|' read -ra BENCHES <<< "$1"
 i=0
 for b in "${BENCHES[@]}"; do
-  timeout -k 10 300 python bench.py $b > gpurun_out/bench_$i.log 2>&1 || { echo "bench $b failed"; tail -30 gpurun_out/bench_$i.log; exit 1; }
+  envs=""; args="$b"
+  if [[ "$b" == *"::"* ]]; then envs="${b%%::*}"; args="${b#*::}"; fi  # "VAR=x VAR2=y::ARGS"
+  timeout -k 10 300 env $envs python bench.py $args > gpurun_out/bench_$i.log 2>&1 || { echo "bench $b failed"; tail -30 gpurun_out/bench_$i.log; exit 1; }
   echo "== $b"; tail -1 gpurun_out/bench_$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('value %.4g ms/step %.4f launch_ms %.4f frac %.3f canon %.3f' % (d['value'], d['ms_per_step'], r['launch_ms'], r['frac'], r['canonical_equiv_frac']), 'step_roof', d['roofline_step'] and round(d['roofline_step']['launch_ms'],4))"
   i=$((i+1))
 done

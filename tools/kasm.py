@@ -21,8 +21,10 @@ def main():
     st = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
     en = next(i for i in range(st, len(lines)) if lines[i].strip().startswith("s_endpgm"))
     open(out, "w").write("\n".join(lines[st:en + 1]))
-    blk = s.split(".name:           " + name)
-    meta = blk[0][blk[0].rfind("  - .agpr_count"):] if len(blk) > 1 else ""
+    i = s.find(".name:           " + name + "\n")
+    j0 = s.rfind("  - .agpr_count", 0, i) if i >= 0 else -1
+    j1 = s.find("  - .agpr_count", i) if i >= 0 else -1
+    meta = s[j0:(j1 if j1 > 0 else len(s))] if i >= 0 else ""
     vg = re.search(r"\.vgpr_count:\s+(\d+)", meta)
     sg = re.search(r"\.sgpr_count:\s+(\d+)", meta)
     body = lines[st:en + 1]
