@@ -1832,7 +1832,9 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 // env's station keys), int cnt[2][B] (per-station connected-UE counts, two steps in flight),
 // int wt[4][16] (per-wave counts: need, active, connected, low QoE), double ps[4][16] (per-wave
 // partial sums: utility, rate, QoE, QoE^2), u128 slot[2] (stream state after the env's last
-// draw, increment), int tab[M] (the env's episode draw table).
+// draw, increment), int tab[M] (the env's episode draw table), double r100[kMaxU + 1]
+// (100 / n correctly rounded: the ResourceFair share without a division, filled once per
+// workgroup).
 struct BlockLds {
   int2* key;
   int* cnt;
@@ -1840,14 +1842,20 @@ struct BlockLds {
   double* ps;
   u128* slot;
   int* tab;
+  double* r100;
 };
 
 // (the keys live in a static array: its 16-byte alignment is known to the compiler, which
 // then reads two stations per broadcast ds_read_b128 -- from the dynamic area it issued four
 // ds_read2_b32, twice the LDS cycles)
+__host__ __device__ inline size_t block_tab_off(int B) {
+  return ((8 * (size_t)B + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32;
+}
+__host__ __device__ inline size_t block_r100_off(int B, int M) {
+  return (block_tab_off(B) + 4 * (size_t)M + 15) & ~(size_t)15;
+}
 __host__ __device__ inline size_t block_lds_bytes(int B, int M) {
-  const size_t cnt = 8 * (size_t)B;
-  return ((cnt + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32 + 4 * (size_t)M;
+  return block_r100_off(B, M) + 8 * (size_t)(kMaxU + 1);
 }
 
 __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
@@ -1861,6 +1869,23 @@ __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   l.slot = reinterpret_cast<u128*>(p + 4 * 64 + 8 * 64);
   l.tab = reinterpret_cast<int*>(p + 4 * 64 + 8 * 64 + 32);
   return l;
+}
+
+__device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B, int M) {
+  BlockLds l = block_lds(base, keys, B);
+  l.r100 = reinterpret_cast<double*>(base + block_r100_off(B, M));
+  return l;
+}
+
+// int32 sum over the 64 lanes of a wavefront (all active), valid in lane 63
+__device__ __forceinline__ int wave_isum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, true);
+  return x;
 }
 
 // The env's steps i0 .. nsteps-1 for one workgroup (block shape); see k_steps_block.
@@ -1905,6 +1930,21 @@ __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& 
   }
 }
 
+// The lean path's row: the per-wave utility sums are 2^-24 fixed-point integers (stored as
+// doubles, exact), summed by the 64 lanes of wave 0 in one DPP tree (exact: integers below
+// 2^53, any order) instead of one lane's chain of dependent LDS reads; lane 63 writes.
+__device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const KOut& out,
+                                                      const BlockLds& L, int nw, int e, int row,
+                                                      const BlockRow& r, int lane) {
+  const double su = wave_sum_f64(lane < nw ? L.ps[lane] : 0.0);
+  if (lane == 63) {
+    const double mean_u = r.nact > 0 ? (su * 0x1p-24) / (double)r.nact : kp.lower;
+    const size_t re = (size_t)row * kp.E + e;
+    out.reward[re] = (float)mean_u;
+    out.done[re] = (uint8_t)(r.t_after >= kp.t_end);
+  }
+}
+
 // nsteps steps of MComCore.step (base.py:230-296) for U > 64: one workgroup of ceil(U/64)
 // waves per env (lane u = UE u), envs e = blockIdx.x, blockIdx.x + gridDim.x, ...; each env's
 // state stays in registers / LDS for the launch (loaded once, stored once) and every step's
@@ -1931,7 +1971,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const bool valid = u < U;
   const uint64_t lt = (1ull << lane) - 1ull;
   const int M = kp.tab_m;
-  const BlockLds L = block_lds(lds_raw, lds_keys, kp.B);
+  const BlockLds L = block_lds(lds_raw, lds_keys, kp.B, kp.tab_m);
+  for (int n = u; n <= U; n += blockDim.x) L.r100[n] = n ? 100.0 / (double)n : 0.0;
   // heterogeneous entities: this UE's class and movement parameters
   const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
   const MoveP mp = HET ? tb.mv[cu]
@@ -2027,8 +2068,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
       const int tot = __builtin_amdgcn_readlane(scan_need, nw - 1);
       const int nact = __builtin_amdgcn_readlane(scan_act, nw - 1);
-      if (u == 0 && i > 0)
-        block_finish_row<LEAN>(kp, out, L, nw, e, traj ? i - 1 : 0, prev);
+      if (LEAN ? (w == 0 && i > 0) : (u == 0 && i > 0)) {
+        if (LEAN) block_finish_row_lean(kp, out, L, nw, e, traj ? i - 1 : 0, prev, lane);
+        else block_finish_row<LEAN>(kp, out, L, nw, e, traj ? i - 1 : 0, prev);
+      }
       int* cnt_next = L.cnt + ((i + 1) & 1) * kp.B;
       for (int k = u; k < kp.B; k += blockDim.x) cnt_next[k] = 0;
 
@@ -2114,12 +2157,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
         if (lane == 0) L.wt[32 + w] = nc;
       }
+      // the rate gather is waited for here, on every path, before this step's stores: a lane or
+      // wave that never reads `full` would carry the load as pending to a later merge, whose
+      // vmcnt(0) (before the register is reused) would then also wait for the stores
+      asm volatile("" ::"v"(full));
       __syncthreads();  // ---- barrier 2
 
       // ---- C: ResourceFair share + rounding, utility, stores, partial sums -------------
       double cents = 0.0;
       float cents_f = 0.f;
-      if (srv >= 0) cents = share_cents(full, cnt[srv], cents_f);
+      if (srv >= 0) {
+        const int n = cnt[srv];
+        cents = share_cents_r(full, L.r100[n], n, cents_f);
+      }
       const bool exact_util = !LEAN;
       const double rate = cents / 100.0;
       double util = 0.0;
@@ -2128,16 +2178,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                           : utility_f32r(cents_f, cents_f * 0.01f, kp);
       const size_t ro = (size_t)row * kp.E * U + idx;
       if (valid) {
-        out.serving[ro] = srv;
-        out.obs[ro] = make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h,
-                                  cents_f * 0.01f, (float)util);
+        // this env's row in the output rows: a wave-uniform base and a 32-bit lane offset
+        const size_t rb = (size_t)row * kp.E * U + (size_t)e * U;
+        at(out.serving + rb, 4u * (uint32_t)u) = srv;
+        at(out.obs + rb, 16u * (uint32_t)u) =
+            make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, cents_f * 0.01f,
+                        (float)util);
         if (!LEAN) {
           if (out.rate64) out.rate64[ro] = rate;
           if (out.util64) out.util64[ro] = active ? util : __builtin_nan("");
         }
       }
-      const double su = wave_sum_f64(active ? util : 0.0);
-      if (lane == 63) L.ps[w] = su;
+      if (LEAN) {  // 2^-24 fixed point: |sum| <= 64 * 2^24 (block_finish_row_lean)
+        const int isu = wave_isum(active ? (int)((float)util * 0x1p24f) : 0);
+        if (lane == 63) L.ps[w] = (double)isu;
+      } else {
+        const double su = wave_sum_f64(active ? util : 0.0);
+        if (lane == 63) L.ps[w] = su;
+      }
       if (!LEAN) {
         const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
         const double sr = wave_sum_f64(srv >= 0 ? rate : 0.0);
@@ -2160,8 +2218,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       t += 1;
     }
     __syncthreads();  // the last step's partial sums
-    if (u == 0 && nsteps > 0)
-      block_finish_row<LEAN>(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev);
+    if (LEAN ? (w == 0 && nsteps > 0) : (u == 0 && nsteps > 0)) {
+      if (LEAN) block_finish_row_lean(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev, lane);
+      else block_finish_row<LEAN>(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev);
+    }
     // ---- epilogue: the state after the last step ----------------------------------------
     if (valid) store_ue(st.ue_state + idx, pos, wp);
     if (u == 0) {
