@@ -248,6 +248,10 @@ __host__ __device__ constexpr ScnConst scn_const(int scn) {
                              MEV_SCN_F32}
        : scn == 2 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 0, 80000, 80576, 113344,
                              MEV_SCN_F32}
+       // mobile-large-perenv-v0: per-env layouts, mode-4 tables of the default channel (rank
+       // index of S at 0, 100/n at 4848, rates at 5424, 46240 bytes)
+       : scn == 3 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 0, 4848, 5424, 46240,
+                             MEV_SCN_F32}
                   : ScnConst{};
 }
 #define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
@@ -1383,7 +1387,7 @@ struct Ctx2 {
   int2 pos, wp;
 };
 
-template <int UC, int SCN, int R>
+template <int UC, int SCN, int R, bool PE>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
                                           const int (&e)[R], const bool (&env_ok)[R],
@@ -1391,7 +1395,8 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                                           const uint64_t (&valid_w)[R], int row,
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
-                                          int* __restrict__ srow, uint8_t* __restrict__ drow) {
+                                          int* __restrict__ srow, uint8_t* __restrict__ drow,
+                                          const int* __restrict__ lkeys) {
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HB = B + 1;
   const int u = m.u;
@@ -1511,10 +1516,39 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       if (arrive[r]) c[r].wp = make_int2(-1, -1);
     }
   }
-  // ---- D: association (mode-3 LDS tables), n_b, share, utility ------------------------------
+  // ---- D: association, n_b, share, utility ---------------------------------------------------
   int srv[R];
   double full[R];
   uint32_t cell[R], ent[R];
+  if (PE) {
+    // per-env layouts: the env's pre-scaled station keys (staged in LDS, see k_steps_packed),
+    // one v_dot2 per station; the full rate at the rank of d2 in S (rank index + rates in LDS)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const s16x2 p2 = {(short)(c[r].pos.x << 1), (short)(c[r].pos.y << 1)};
+      const v4u32* sv = reinterpret_cast<const v4u32*>(lkeys + (r * G + m.seg) * 32);
+      unsigned best = UINT_MAX;
+      auto scan = [&](auto npair) {
+#pragma unroll
+        for (int q = 0; q < decltype(npair)::value; ++q) {
+          const v4u32 w = sv[q];
+          const unsigned k0 = (unsigned)__builtin_amdgcn_sdot2(p2, as_s16x2(w.x), (int)w.y, false);
+          const unsigned k1 = (unsigned)__builtin_amdgcn_sdot2(p2, as_s16x2(w.z), (int)w.w, false);
+          best = min(best, min(k0, k1));
+        }
+      };
+      if (KPS(B) <= 8) scan(std::integral_constant<int, 4>());
+      else scan(std::integral_constant<int, 8>());
+      const int d2s = (int)(best >> 4) - (1 << 21) + __mul24(c[r].pos.x, c[r].pos.x) +
+                      __mul24(c[r].pos.y, c[r].pos.y);
+      srv[r] = active[r] && best != UINT_MAX && d2s <= kp.d2max ? (int)(best & 15u) : -1;
+      const uint32_t dq = (uint32_t)min(max(d2s, 0), kp.d2max);
+      const uint2 w = *reinterpret_cast<const uint2*>(lblob + 8u * (dq >> 5));  // (mode 4: at 0)
+      const uint32_t k = w.y + (uint32_t)__popc(w.x & ((1u << (dq & 31u)) - 1u));
+      full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
+      cell[r] = ent[r] = 0;
+    }
+  } else {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     cell[r] = min((uint32_t)(__mul24(c[r].pos.y, KPS(W)) + c[r].pos.x),
@@ -1523,9 +1557,10 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent[r] & 4095u));
     srv[r] = active[r] && ent[r] < 0xF000u ? (int)(ent[r] >> 12) : -1;
   }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    if (bal(ent[r] == 0xFFFFu) & act_w[r]) {  // cells beyond the table's ranks: L2 map
+    if (!PE && (bal(ent[r] == 0xFFFFu) & act_w[r])) {  // cells beyond the table's ranks: L2 map
       if (active[r] && ent[r] == 0xFFFFu) {
         const int4 q = at(const_cast<int4*>(tb.assoc), 16u * cell[r]);
         srv[r] = q.x;
@@ -1619,13 +1654,15 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
   __syncthreads();
 }
 
-// LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, histograms [R G][B + 1] int, draw
-// tables [R G][M] int
-__host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R) {
-  return sizeof(int) * (size_t)(R * G) * (8 + (size_t)(B + 1) + (size_t)M);
+// LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, (PE) station keys [R G][16][2] int,
+// histograms [R G][B + 1] int, draw tables [R G][M] int
+__host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool PE = false) {
+  return sizeof(int) * (size_t)(R * G) * (8 + (PE ? 32 : 0) + (size_t)(B + 1) + (size_t)M);
 }
 
-template <int UC, int SCN>
+// PE: per-env station layouts (KParams::lds_mode 4: the blob holds the rank index of S, 100/n
+// and rate_full over S; the env's station keys are staged per launch like k_steps_packed's)
+template <int UC, int SCN, bool PE = false>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -1649,10 +1686,12 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const int lane = threadIdx.x & 63;
   const LaneMap m = lane_map<PC>(lane, PC);
   int* lw = lds_all + (KPS(lds_assoc) >> 2);
+  constexpr int KB = PE ? 32 : 0;  // ints per env of staged station keys
   u128* lpcg = reinterpret_cast<u128*>(lw) + wv * R * G * 2;
-  int* hist = lw + NW * R * G * 8 + wv * R * G * (B + 1);
-  int* ltab = lw + NW * R * G * (8 + B + 1) + wv * R * G * M;
-  int* srow = lw + NW * R * G * (8 + B + 1 + M);
+  int* lkeys = lw + NW * R * G * 8 + wv * R * G * KB;
+  int* hist = lw + NW * R * G * (8 + KB) + wv * R * G * (B + 1);
+  int* ltab = lw + NW * R * G * (8 + KB + B + 1) + wv * R * G * M;
+  int* srow = lw + NW * R * G * (8 + KB + B + 1 + M);
   uint8_t* drow = reinterpret_cast<uint8_t*>(srow + stage_rows * NWG);
   const int npairs = (ngroups + 1) / 2;
   const int gstride = (int)gridDim.x * NW;
@@ -1691,6 +1730,20 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       c[r].pos = make_int2(a.s.x, a.s.y);
       c[r].wp = make_int2(a.s.z, a.s.w);
       pa[r] = pbv[r] = make_ulonglong2(0, 0);
+      if (PE && m.seg < G) {  // the env's station keys (see k_steps_packed's staging)
+        const int ec = min(e[r], kp.E - 1);
+        const int nbf = env_ok[r] ? (st.bs_count ? st.bs_count[ec] : B) : 0;
+        for (int k = m.u; k < 16; k += PC) {
+          int2 kv = make_int2(0, -1);
+          if (k < nbf) {
+            const int2 q = st.bs_xy[(size_t)ec * B + k];
+            const s16x2 m2 = {(short)(-16 * q.x), (short)(-16 * q.y)};
+            kv = make_int2(__builtin_bit_cast(int, m2),
+                           (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << 4) | (unsigned)k));
+          }
+          *reinterpret_cast<int2*>(lkeys + (r * G + m.seg) * 32 + 2 * k) = kv;
+        }
+      }
       if (env_ok[r] && leader) {
         ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
         pa[r] = at(pr, 48u * (uint32_t)e[r]);
@@ -1711,9 +1764,9 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     __builtin_amdgcn_s_waitcnt(0);
     for (int i = 0; i < nsteps; ++i) {
       const int sr = i % stage_rows;
-      lds2_step<UC, SCN, R>(kp, st, out, tb, m, c, e, env_ok, envok_w, valid_w, traj ? i : 0, lblob,
-                            lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
-                            drow + sr * NWG + wvu * G * R);
+      lds2_step<UC, SCN, R, PE>(kp, st, out, tb, m, c, e, env_ok, envok_w, valid_w, traj ? i : 0,
+                                lblob, lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
+                                drow + sr * NWG + wvu * G * R, lkeys);
       if (sr == stage_rows - 1 || i == nsteps - 1)
         flush_staged2(out, srow, drow, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG);
     }
@@ -2551,12 +2604,13 @@ static unsigned fbits(float f) {
 static int match_scn(const mev_ctx* ctx) {
   if (!ctx->scn_allowed) return 0;
   const KParams& kp = ctx->kp;
-  for (int s = 1; s <= 2; ++s) {
+  for (int s = 1; s <= 3; ++s) {
     const ScnConst c = scn_const(s);
+    if ((s == 3) != (ctx->p.bs_per_env != 0)) continue;
     if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
         kp.hist_lds == c.hist_lds && kp.t_end == c.t_end && kp.arr_start == c.arr_start &&
         kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
-        kp.lds_mode == 3 &&
+        kp.lds_mode == (s == 3 ? 4 : 3) &&
         kp.lds_r100_off == c.lds_r100_off && kp.lds_rate_off == c.lds_rate_off &&
         kp.lds_assoc == c.lds_assoc && kp.d2snap == c.d2snap && kp.axis_exact == c.axis_exact &&
         fbits(kp.vel_f) == c.vel_f && fbits(kp.move_lim) == c.move_lim &&
@@ -2588,14 +2642,23 @@ static size_t stage_lds_bytes(const KParams& kp, int rows, int nw) {
 // UE to a station is a sum of two squares, so rank(d2) indexes the compact rate array for every
 // connectable pair. The layout part (cell map, stations) is written by mev_update_stations.
 // Leaves c->blob null (the kernel then gathers from `assoc`) when the shape does not qualify:
-// per-env layouts, more than 15 stations, U > 64, or tables larger than one workgroup's share.
+// more than 15 stations (shared) / 16 (per-env), U > 64, or tables larger than one workgroup's
+// share. Per-env layouts get mode 4 (rank index, 100/n, rates over S) for k_steps_lds2.
 static int build_lds_tables(mev_ctx* c) {
   KParams& kp = c->kp;
   kp.lds_assoc = 0;
   kp.lds_mode = 0;
   const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 / 3 force a mode
   const int want = sw ? atoi(sw) : 3;
-  if (want == 0 || c->p.bs_per_env || kp.B > 15 || kp.U > 64 || c->d2max < 0) return MEV_OK;
+  if (want == 0 || kp.U > 64 || c->d2max < 0) return MEV_OK;
+  // per-env layouts (mode 4): the layout-independent rank index of S, 100/n and the rates over
+  // S for the two-group kernel (k_steps_lds2<U, 0, true>); the station keys are staged per launch
+  const char* l2e = getenv("MEV_LDS2");  // dev / test switch: 0 = one group per wavefront
+  const bool lds2_off = l2e && atoi(l2e) == 0;
+  if (c->p.bs_per_env &&
+      !(kp.B <= 16 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !lds2_off))
+    return MEV_OK;
+  if (!c->p.bs_per_env && kp.B > 15) return MEV_OK;
   const int cells = kp.W * kp.H;
   const int d2max = c->d2max;
   const size_t nwords = (size_t)d2max / 32 + 1;
@@ -2622,6 +2685,45 @@ static int build_lds_tables(mev_ctx* c) {
   // [rank index][100/n][rates]
   size_t st_off = 0, rank_off = 0, r16_off = 0, r100_off, rate_off, total;
   int mode = 0;
+  if (c->p.bs_per_env) {
+    r100_off = up16(8 * nwords);
+    rate_off = r100_off + 8 * 72;
+    total = up16(rate_off + 8 * (size_t)count);
+    const int G = kp.envs_per_wave;
+    const size_t sh2 = total + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2, true);
+    const size_t row2 = (size_t)kLds2Waves * G * 2 * 5;
+    if (sh2 + row2 + 4 > (size_t)kLds2BytesPerWG) return MEV_OK;
+    std::vector<double> fullp((size_t)d2max + 1);
+    MEV_HIP(hipMemcpy(fullp.data(), c->rate_full, sizeof(double) * fullp.size(),
+                      hipMemcpyDeviceToHost));
+    std::vector<char> host(total, 0);
+    memcpy(host.data(), rank.data(), 8 * nwords);
+    double* r100p = reinterpret_cast<double*>(host.data() + r100_off);
+    for (int n = 1; n <= 64; ++n) r100p[n] = 100.0 / (double)n;
+    double* ratesp = reinterpret_cast<double*>(host.data() + rate_off);
+    for (int d = 0, k = 0; d <= d2max; ++d)
+      if ((bits[(size_t)d >> 5] >> (d & 31)) & 1u) ratesp[k++] = fullp[(size_t)d];
+    if (hipMalloc(&c->blob, total) != hipSuccess) return MEV_ENOMEM;
+    MEV_HIP(hipMemcpy(c->blob, host.data(), total, hipMemcpyHostToDevice));
+    kp.lds_assoc = (int)total;
+    kp.lds_mode = 4;
+    kp.lds_rank_off = 0;
+    kp.lds_r100_off = (int)r100_off;
+    kp.lds_rate_off = (int)rate_off;
+    c->stage_cap = 0;
+    if (const char* sr = getenv("MEV_STAGE_ROWS"))
+      if (atoi(sr) > 0) c->stage_cap = atoi(sr);
+    c->stage_rows2 = (int)(((size_t)kLds2BytesPerWG - sh2 - 4) / row2);
+    if (c->stage_cap > 0) c->stage_rows2 = std::min(c->stage_rows2, c->stage_cap);
+    int cus = 0, n2 = 0;
+    MEV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n2, reinterpret_cast<const void*>(kp.U == 15 ? k_steps_lds2<15, 0, true>
+                                                      : k_steps_lds2<30, 0, true>),
+        64 * kLds2Waves, sh2 + (((size_t)c->stage_rows2 * row2 + 3) & ~(size_t)3)));
+    c->lds2_wgs = cus * n2;
+    return MEV_OK;
+  }
   // mode 3 for aligned env segments (U -> 16 / 32 lanes); measured slower than mode 1 for
   // mobile-small (U = 5: 162 vs 142 us per 40-step launch at 65,536 envs)
   const bool aligned = pitch_of(kp.U) == 16 || pitch_of(kp.U) == 32;
@@ -2708,8 +2810,7 @@ static int build_lds_tables(mev_ctx* c) {
   c->lds_wgs = cus * per;
   // two env groups per wavefront (k_steps_lds2): mode 3, U = 15 / 30, a draw table
   c->lds2_wgs = 0;
-  const char* l2 = getenv("MEV_LDS2");  // dev / test switch: 0 = one group per wavefront
-  if (mode == 3 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !(l2 && atoi(l2) == 0)) {
+  if (mode == 3 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !lds2_off) {
     const int G = kp.envs_per_wave;
     const size_t sh2 = total + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2);
     const size_t row2 = (size_t)kLds2Waves * G * 2 * 5;
@@ -3034,6 +3135,8 @@ int mev_create(const mev_params* params, mev_ctx** out) {
       return MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(c->assoc, 0xff, bytes));  // srv -1 everywhere until a layout is set
+  }
+  if (!c->kp.het) {  // LDS tables: shared layouts (modes 1-3), per-env layouts (mode 4)
     rc = build_lds_tables(c);
     if (rc) {
       mev_destroy(c);
@@ -3115,7 +3218,8 @@ const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullp
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
   const bool lean_ok = !c->kp.util_direct;
-  return (c->kp.lds_assoc > 0 && c->kp.lds_mode == 3 && !c->p.bs_per_env && lean_ok)
+  return (c->kp.lds_assoc > 0 && lean_ok &&
+          ((c->kp.lds_mode == 3 && !c->p.bs_per_env) || (c->kp.lds_mode == 4 && c->p.bs_per_env)))
              ? match_scn(c) : 0;
 }
 
@@ -3217,6 +3321,22 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const int ldsm = ldsa ? kp.lds_mode : 0;
     // two env groups per wavefront when the batch fills every resident workgroup with them
     const int pairs = (groups + 1) / 2;
+    if (c->p.bs_per_env && kp.lds_mode == 4 && lean && traj && c->lds2_wgs > 0 &&
+        pairs >= c->lds2_wgs * kLds2Waves) {  // per-env layouts (k_steps_lds2<U, 0, true>)
+      StepsKernel k2 = kp.U == 15 ? k_steps_lds2<15, 0, true>
+                                  : (match_scn(c) == 3 ? k_steps_lds2<30, 3, true>
+                                                       : k_steps_lds2<30, 0, true>);
+      const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
+      const int G = kp.envs_per_wave;
+      const int srows = std::min(c->stage_rows2, nsteps);
+      const size_t sh = (size_t)kp.lds_assoc +
+                        kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2, true) +
+                        (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
+      k2<<<dim3(blocks), dim3(64 * kLds2Waves), sh, stream>>>(kp, ks, ko, tb, groups, nsteps, 1,
+                                                              srows);
+      MEV_HIP(hipGetLastError());
+      return MEV_OK;
+    }
     if (ldsm == 3 && lean && c->lds2_wgs > 0 && pairs >= c->lds2_wgs * kLds2Waves) {
       const int scn = match_scn(c);
       StepsKernel k2 = kp.U == 15 ? (scn == 1 ? k_steps_lds2<15, 1> : k_steps_lds2<15, 0>)
