@@ -1762,8 +1762,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       valid_w[r] = bal(env_ok[r] && m.u < U);
     }
     __builtin_amdgcn_s_waitcnt(0);
-    for (int i = 0; i < nsteps; ++i) {
-      const int sr = i % stage_rows;
+    for (int i = 0, sr = 0; i < nsteps; ++i, sr = sr + 1 == stage_rows ? 0 : sr + 1) {
       lds2_step<UC, SCN, R, PE>(kp, st, out, tb, m, c, e, env_ok, envok_w, valid_w, traj ? i : 0,
                                 lblob, lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
                                 drow + sr * NWG + wvu * G * R, lkeys);
