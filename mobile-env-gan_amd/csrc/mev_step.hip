@@ -1390,9 +1390,8 @@ struct Ctx2 {
 template <int UC, int SCN, int R, bool PE>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
-                                          const int (&e)[R], const bool (&env_ok)[R],
-                                          const uint64_t (&envok_w)[R],
-                                          const uint64_t (&valid_w)[R], int row,
+                                          const int (&e)[R], const int (&nok)[R], int kval,
+                                          int klead, int row,
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
                                           int* __restrict__ srow, uint8_t* __restrict__ drow,
@@ -1400,7 +1399,24 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HB = B + 1;
   const int u = m.u;
-  const bool lead_lane = u == PC - 1;
+  // lanes UE u of segment s hold valid = u < U; wave masks of the envs that exist (nok[r] of
+  // the group's G) from the uniform count, in SALU each step (kept loop-variant: hoisted, the
+  // masks would be spilled from SGPRs and restored by v_readlane every step)
+  constexpr uint64_t kValidPat = [] {
+    uint64_t v = 0;
+    for (int q = 0; q < 64 / PC; ++q) v |= ((1ull << U) - 1ull) << (q * PC);
+    return v;
+  }();
+  bool env_ok[R];
+  uint64_t envok_w[R], valid_w[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int nk = nok[r];
+    asm volatile("" : "+s"(nk));
+    envok_w[r] = nk >= G ? ~0ull : ((1ull << (uint32_t)(nk * PC)) - 1ull);
+    valid_w[r] = envok_w[r] & kValidPat;
+    env_ok[r] = m.seg < nk;
+  }
   bool valid[R], active[R], need[R], do_reset[R], reset_env[R];
   int tot[R], rank[R];
   uint64_t act_w[R], mneed_w[R];
@@ -1408,7 +1424,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int er = r * G + m.seg;  // the env's slot among the wave's R * G
-    valid[r] = env_ok[r] && u < U;
+    valid[r] = kval < nok[r];
     reset_env[r] = env_ok[r] && c[r].t >= KPS(t_end);
     do_reset[r] = reset_env[r] && valid[r];
     if (bal(c[r].t >= KPS(t_end)) & envok_w[r]) {  // initial positions = the episode's first U
@@ -1623,7 +1639,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // the env's staged row entry: the 2^-25 fixed-point utility sum and {nact, done}; the
     // workgroup's flush forms the float32 reward from them. Lanes other than the env's last
     // write into the histogram's spare bin instead (no branch).
-    const bool lead = env_ok[r] && lead_lane;
+    const bool lead = klead < nok[r];
     const int er = r * G + m.seg;
     int* sw = lead ? srow + er : h[r] + B;
     uint8_t* dw = lead ? drow + er : reinterpret_cast<uint8_t*>(h[r] + B);
@@ -1706,9 +1722,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       continue;
     }
     Ctx2 c[R];
-    int e[R];
+    int e[R], nok[R];
     bool env_ok[R];
-    uint64_t envok_w[R], valid_w[R];
     ulonglong2 pa[R], pbv[R];
     const bool leader = m.u == PC - 1;
 #pragma unroll
@@ -1716,6 +1731,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       const int g = 2 * p + r;
       e[r] = g * G + m.seg;
       env_ok[r] = (m.seg < G) && (e[r] < kp.E);
+      nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
       // the group's draw tables (LDS-DMA) and state, issued before one wait
       const int nt = G * M;
       const int lim = max(0, min(nt, (kp.E - g * G) * M));
@@ -1758,15 +1774,14 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         lpcg[2 * (r * G + m.seg)] = mk128(pa[r].x, pa[r].y);
         lpcg[2 * (r * G + m.seg) + 1] = mk128(pbv[r].x, pbv[r].y);
       }
-      envok_w[r] = bal(env_ok[r]);
-      valid_w[r] = bal(env_ok[r] && m.u < U);
     }
+    const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
     __builtin_amdgcn_s_waitcnt(0);
     for (int i = 0, sr = 0; i < nsteps; ++i, sr = sr + 1 == stage_rows ? 0 : sr + 1) {
-      lds2_step<UC, SCN, R, PE>(kp, st, out, tb, m, c, e, env_ok, envok_w, valid_w, traj ? i : 0,
+      lds2_step<UC, SCN, R, PE>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
                                 lblob, lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
                                 drow + sr * NWG + wvu * G * R, lkeys);
-      if (sr == stage_rows - 1 || i == nsteps - 1)
+      if (sr + 1 == stage_rows || i + 1 == nsteps)
         flush_staged2(out, srow, drow, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG);
     }
     // the state after the last step (see k_steps_packed)
