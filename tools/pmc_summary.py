@@ -27,7 +27,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CHUNK = 40  # bench.py default --chunk: steps per engine call (rollout launch)
+CHUNK = 200  # bench.py default --chunk: steps per engine call (rollout launch)
 
 FUSED_RE = re.compile(r"k_steps_packed<|k_steps_block<|k_steps_lds2<")
 SINGLE_RE = re.compile(r"k_step_packed<|k_steps_block<")
