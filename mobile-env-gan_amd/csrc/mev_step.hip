@@ -238,10 +238,11 @@ struct ScnConst {
   int d2snap, axis_exact;
   unsigned vel_f, move_lim, inv_w, inv_h, u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale,
       u_offset;
+  int d2max;
 };
 __host__ __device__ constexpr ScnConst scn_const(int scn) {
 #define MEV_SCN_F32 2, 1, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
-                    0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u
+                    0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u, 19362
   // (LDS tables of mode 3 for 200 x 200: cell entries [0, 80000), 100/n at 80000, rates at
   // 80576, 113344 bytes in all)
   return scn == 1 ? ScnConst{15, 7, 200, 200, 53, 1, 20, 0, 20, 1, 0, 80000, 80576, 113344,
@@ -252,6 +253,12 @@ __host__ __device__ constexpr ScnConst scn_const(int scn) {
        // index of S at 0, 100/n at 4848, rates at 5424, 46240 bytes)
        : scn == 3 ? ScnConst{30, 13, 200, 200, 98, 1, 20, 0, 20, 1, 0, 4848, 5424, 46240,
                              MEV_SCN_F32}
+       // mobile-custom-128x1024-v0 (block kernel): velocity 10 (d2snap 100, float32 10, tie
+       // band 2^-16 x 10), draw table 3U + 8, no LDS tables, default channel and utility
+       : scn == 4 ? ScnConst{1024, 128, 200, 200, 3080, 0, 20, 0, 20, 1, 0, 0, 0, 0, 100, 1,
+                             0x41200000u, 0x3effec00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u,
+                             0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u,
+                             19362}
                   : ScnConst{};
 }
 #define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
@@ -2025,25 +2032,25 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
 //   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums
 // The per-station counts alternate between two LDS arrays (the next step's array is zeroed
 // in its B phase), so two barriers per step suffice.
-template <bool PER_ENV_BS, bool LEAN, bool HET>
+template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
   extern __shared__ __align__(16) char lds_raw[];
   __shared__ __align__(16) int2 lds_keys[kMaxB + 2 + kMaxClasses];
   const int u = threadIdx.x;
-  const int U = kp.U;
+  const int U = KPS(U);
   const int lane = u & 63;
   const int w = u >> 6;
   const int nw = (blockDim.x + 63) >> 6;
   const bool valid = u < U;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const int M = kp.tab_m;
-  const BlockLds L = block_lds(lds_raw, lds_keys, kp.B, kp.tab_m);
+  const int M = KPS(tab_m);
+  const BlockLds L = block_lds(lds_raw, lds_keys, KPS(B), KPS(tab_m));
   for (int n = u; n <= U; n += blockDim.x) L.r100[n] = n ? 100.0 / (double)n : 0.0;
   // heterogeneous entities: this UE's class and movement parameters
   const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
   const MoveP mp = HET ? tb.mv[cu]
-                       : MoveP{kp.vel, kp.vel_f, kp.move_lim, kp.d2snap, kp.axis_exact};
+                       : MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)};
   for (int e = blockIdx.x; e < kp.E; e += gridDim.x) {
     // ---- prologue: state, stream, station keys, draw table -------------------------------
     const size_t idx = (size_t)e * U + u;
@@ -2060,11 +2067,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       L.slot[0] = mk128(pr[0].x, pr[0].y);
       L.slot[1] = mk128(pr[1].x, pr[1].y);
     }
-    const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : kp.B) : kp.B;
+    const int nb = PER_ENV_BS ? (st.bs_count ? st.bs_count[e] : KPS(B)) : KPS(B);
     // station keys {m as int16x2, c = ((|q|^2 + 2^21) << 10) | j}: with the map <= 512 x 512 and
     // every station in [0, 512)^2, m = -64 q and key = dot2(32 p, m) + c =
     // ((|p - q|^2 - |p|^2 + 2^21) << 10) | j; otherwise m = -2 q, key = (dot2(p, m) << 10) + c
-    const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * kp.B : st.bs_xy;
+    const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * KPS(B) : st.bs_xy;
     bool in512 = true;
     for (int i = u; i < nb; i += blockDim.x) {
       const int2 qq = bsx[i];
@@ -2072,7 +2079,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
     if (M)
       for (int k = u; k < M; k += blockDim.x) L.tab[k] = tb.tab_xy[(size_t)e * M + k];
-    const bool scaled = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512;
+    const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
     // and stations beyond the env's count get the key that never wins, m = 0, c = UINT_MAX)
     const int nslot = HET ? kp.bperm : nb;
@@ -2089,16 +2096,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                               (int)(((unsigned)(qq.x * qq.x + qq.y * qq.y + (1 << 21)) << kKeyBits) |
                                     (unsigned)i));
     }
-    for (int i = u; i < kp.B; i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
+    for (int i = u; i < KPS(B); i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
     bool s_ok = true;  // the slot holds the state after the env's last draw
     BlockRow prev{0, 0, 0};
     __syncthreads();
 
     for (int i = 0; i < nsteps; ++i) {
       const int row = traj ? i : 0;
-      int* cnt = L.cnt + (i & 1) * kp.B;  // (B = count array stride; two arrays below)
+      int* cnt = L.cnt + (i & 1) * KPS(B);  // (B = count array stride; two arrays below)
       // ---- A: lazy auto-reset, ballots ------------------------------------------------
-      const bool reset = t >= kp.t_end;  // uniform
+      const bool reset = t >= KPS(t_end);  // uniform
       int koff = 0;
       u128 base = L.slot[0];  // read before barrier 1 (the slot is written after it)
       const u128 inc = L.slot[1];
@@ -2119,8 +2126,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           koff = 2 * U;
         }
       }
-      const bool active = valid && t >= kp.arr_start && t < kp.arr_exit &&
-                          (kp.first_step_active || t != 0);
+      const bool active = valid && t >= KPS(arr_start) && t < KPS(arr_exit) &&
+                          (KPS(first_step_active) || t != 0);
       const bool need = active && wp.x < 0;
       const uint64_t mneed = bal(need);
       const uint64_t mact = bal(active);
@@ -2139,8 +2146,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         if (LEAN) block_finish_row_lean(kp, out, L, nw, e, traj ? i - 1 : 0, prev, lane);
         else block_finish_row<LEAN>(kp, out, L, nw, e, traj ? i - 1 : 0, prev);
       }
-      int* cnt_next = L.cnt + ((i + 1) & 1) * kp.B;
-      for (int k = u; k < kp.B; k += blockDim.x) cnt_next[k] = 0;
+      int* cnt_next = L.cnt + ((i + 1) & 1) * KPS(B);
+      for (int k = u; k < KPS(B); k += blockDim.x) cnt_next[k] = 0;
 
       // ---- B: waypoint draws in ue_id order (movement.py:44-47), move ------------------
       const int rank = pre_need + (int)__popcll(mneed & lt);
@@ -2200,8 +2207,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           }
         }
         d2s = key_d2(best, pos);
-        if (best != UINT_MAX && d2s <= kp.d2max) srv = (int)(best & ((1u << kKeyBits) - 1));
-        full = tb.rate_full[max(0, min(d2s, kp.d2max))];
+        if (best != UINT_MAX && d2s <= KPS(d2max)) srv = (int)(best & ((1u << kKeyBits) - 1));
+        full = tb.rate_full[max(0, min(d2s, KPS(d2max)))];
       } else {
         // per station class: the class's closest station, connectable iff d2 <= d2max of the
         // (station class, this UE's class) pair -- the closest connectable station overall is
@@ -2242,14 +2249,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       double util = 0.0;
       if (active)
         util = exact_util ? utility_of(rate, cents, kp, tb.util)
-                          : utility_f32r(cents_f, cents_f * 0.01f, kp);
+                          : utility_f32r<SCN>(cents_f, cents_f * 0.01f, kp);
       const size_t ro = (size_t)row * kp.E * U + idx;
       if (valid) {
         // this env's row in the output rows: a wave-uniform base and a 32-bit lane offset
         const size_t rb = (size_t)row * kp.E * U + (size_t)e * U;
         at(out.serving + rb, 4u * (uint32_t)u) = srv;
         at(out.obs + rb, 16u * (uint32_t)u) =
-            make_float4((float)pos.x * kp.inv_w, (float)pos.y * kp.inv_h, cents_f * 0.01f,
+            make_float4((float)pos.x * KPSF(inv_w), (float)pos.y * KPSF(inv_h), cents_f * 0.01f,
                         (float)util);
         if (!LEAN) {
           if (out.rate64) out.rate64[ro] = rate;
@@ -2618,13 +2625,14 @@ static unsigned fbits(float f) {
 static int match_scn(const mev_ctx* ctx) {
   if (!ctx->scn_allowed) return 0;
   const KParams& kp = ctx->kp;
-  for (int s = 1; s <= 3; ++s) {
+  for (int s = 1; s <= 4; ++s) {
     const ScnConst c = scn_const(s);
-    if ((s == 3) != (ctx->p.bs_per_env != 0)) continue;
+    if ((s >= 3) != (ctx->p.bs_per_env != 0)) continue;
+    if ((s == 4) != (kp.U > 64) || kp.het) continue;
     if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
         kp.hist_lds == c.hist_lds && kp.t_end == c.t_end && kp.arr_start == c.arr_start &&
         kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
-        kp.lds_mode == (s == 3 ? 4 : 3) &&
+        kp.lds_mode == (s == 4 ? 0 : s == 3 ? 4 : 3) && kp.d2max == c.d2max &&
         kp.lds_r100_off == c.lds_r100_off && kp.lds_rate_off == c.lds_rate_off &&
         kp.lds_assoc == c.lds_assoc && kp.d2snap == c.d2snap && kp.axis_exact == c.axis_exact &&
         fbits(kp.vel_f) == c.vel_f && fbits(kp.move_lim) == c.move_lim &&
@@ -3232,8 +3240,9 @@ const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullp
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
   const bool lean_ok = !c->kp.util_direct;
-  return (c->kp.lds_assoc > 0 && lean_ok &&
-          ((c->kp.lds_mode == 3 && !c->p.bs_per_env) || (c->kp.lds_mode == 4 && c->p.bs_per_env)))
+  return (lean_ok && ((c->kp.lds_assoc > 0 && ((c->kp.lds_mode == 3 && !c->p.bs_per_env) ||
+                                                (c->kp.lds_mode == 4 && c->p.bs_per_env))) ||
+                      (c->kp.U > 64 && c->p.bs_per_env && !c->kp.het)))
              ? match_scn(c) : 0;
 }
 
@@ -3426,6 +3435,8 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                         : (lean ? k_steps_block<false, true, true> : k_steps_block<false, false, true>))
              : (per_env ? (lean ? k_steps_block<true, true, false> : k_steps_block<true, false, false>)
                         : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
+  if (lean && per_env && !kp.het && match_scn(c) == 4)  // mobile-custom-128x1024's constants
+    kf = k_steps_block<true, true, false, 4>;
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
   const size_t shm = block_lds_bytes(kp.B, kp.tab_m);
   if (c->fuse_steps || nsteps == 1) {
