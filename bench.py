@@ -205,6 +205,9 @@ def main():
                          "env-steps/s -- the per-launch tail and the per-group prologue amortised)")
     ap.add_argument("--step-launches", type=int, default=200,
                     help="one-step launches timed after the timed region for roofline_step")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine launch-shape override (EngineParams: lds_tables, two_groups, "
+                         "stage_rows, xcd_remap, scenario_constants), for A/B runs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no step roofline)")
@@ -242,9 +245,10 @@ def main():
 
     E = args.envs
     seeds = shard_seeds(1000, E, rank)  # rank r owns global envs [r*E, (r+1)*E)
+    overrides = {k: int(v) for k, v in (kv.split("=", 1) for kv in args.engine)}
     env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
                           stream_split=2 if args.launch == "split" else 0,
-                          fuse_steps=0 if args.launch == "fused" else -1)
+                          fuse_steps=0 if args.launch == "fused" else -1, **overrides)
     eng = env.engine
     U, B = env.num_ues, env.num_bs
     per_env_bs = eng.bs_per_env

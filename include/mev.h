@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 10
+#define MEV_ABI_VERSION 11
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -120,6 +120,17 @@ typedef struct mev_params {
   const double* bs_class_params;
   const double* ue_class_params;
   const int64_t* rate_table_offsets;
+  /* Launch-shape overrides, for tests and A/B measurements (0 everywhere = automatic: the
+   * fastest shape the context qualifies for). Results are identical for every setting.
+   *   lds_tables: rollouts of a shared layout read the association from LDS tables of mode
+   *     1..3 (KTables::lds_blob in mev_step.hip), -1: from the L2 association map;
+   *   two_groups: -1: one env group per wavefront in rollout launches (else two where the
+   *     batch fills the GPU with pairs);
+   *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
+   *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges);
+   *   scenario_constants: -1: the generic kernel instances only (else a registered scenario's
+   *     parameters are compiled in when every value matches). */
+  int32_t lds_tables, two_groups, stage_rows, xcd_remap, scenario_constants;
 } mev_params;
 
 typedef struct mev_state {

@@ -2670,13 +2670,14 @@ static int build_lds_tables(mev_ctx* c) {
   KParams& kp = c->kp;
   kp.lds_assoc = 0;
   kp.lds_mode = 0;
-  const char* sw = getenv("MEV_LDS_ASSOC");  // dev A/B switch: 0 off, 1 / 2 / 3 force a mode
-  const int want = sw ? atoi(sw) : 3;
+  // mev_params.lds_tables: 0 auto (mode 3 where it applies), -1 none, 1..3 force a mode
+  const int lt = c->p.lds_tables;
+  const bool forced = lt > 0;
+  const int want = lt < 0 ? 0 : lt > 0 ? std::min(lt, 3) : 3;
   if (want == 0 || kp.U > 64 || c->d2max < 0) return MEV_OK;
   // per-env layouts (mode 4): the layout-independent rank index of S, 100/n and the rates over
   // S for the two-group kernel (k_steps_lds2<U, 0, true>); the station keys are staged per launch
-  const char* l2e = getenv("MEV_LDS2");  // dev / test switch: 0 = one group per wavefront
-  const bool lds2_off = l2e && atoi(l2e) == 0;
+  const bool lds2_off = c->p.two_groups < 0;  // mev_params.two_groups
   if (c->p.bs_per_env &&
       !(kp.B <= 16 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !lds2_off))
     return MEV_OK;
@@ -2732,9 +2733,7 @@ static int build_lds_tables(mev_ctx* c) {
     kp.lds_rank_off = 0;
     kp.lds_r100_off = (int)r100_off;
     kp.lds_rate_off = (int)rate_off;
-    c->stage_cap = 0;
-    if (const char* sr = getenv("MEV_STAGE_ROWS"))
-      if (atoi(sr) > 0) c->stage_cap = atoi(sr);
+    c->stage_cap = c->p.stage_rows > 0 ? c->p.stage_rows : 0;
     c->stage_rows2 = (int)(((size_t)kLds2BytesPerWG - sh2 - 4) / row2);
     if (c->stage_cap > 0) c->stage_rows2 = std::min(c->stage_rows2, c->stage_cap);
     int cus = 0, n2 = 0;
@@ -2749,7 +2748,7 @@ static int build_lds_tables(mev_ctx* c) {
   // mode 3 for aligned env segments (U -> 16 / 32 lanes); measured slower than mode 1 for
   // mobile-small (U = 5: 162 vs 142 us per 40-step launch at 65,536 envs)
   const bool aligned = pitch_of(kp.U) == 16 || pitch_of(kp.U) == 32;
-  if (want >= 3 && cells <= 65536 && (aligned || (sw && want == 3))) {  // [cell entries u16][100/n][rates over D]
+  if (want >= 3 && cells <= 65536 && (aligned || forced)) {  // [cell entries u16][100/n][rates over D]
     r100_off = up16(2 * (size_t)cells);
     rate_off = r100_off + 8 * 72;
     total = up16(rate_off + 8 * (size_t)kLds3Rates);
@@ -2815,12 +2814,8 @@ static int build_lds_tables(mev_ctx* c) {
   c->stage_rows = mode >= 2 ? (int)(((size_t)kLds2BytesPerWG - shmem - 4) /
                                     (nw * stage_bytes_per_row(kp)))
                             : 0;
-  c->stage_cap = 0;
-  if (const char* sr = getenv("MEV_STAGE_ROWS"))  // test switch: shorter staging windows
-    if (atoi(sr) > 0) {
-      c->stage_cap = atoi(sr);
-      c->stage_rows = std::min(c->stage_rows, c->stage_cap);
-    }
+  c->stage_cap = c->p.stage_rows > 0 ? c->p.stage_rows : 0;  // shorter staging windows
+  if (c->stage_cap > 0) c->stage_rows = std::min(c->stage_rows, c->stage_cap);
   int per = 1 << 30;
   for (int lean = 0; lean < 2; ++lean) {
     int n = 0;
@@ -3059,10 +3054,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.u_upperf = (float)kp.upper;
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
-  {
-    const char* xr = getenv("MEV_XCD_REMAP");  // dev A/B switch
-    kp.xcd_remap = xr ? atoi(xr) : 1;
-  }
+  kp.xcd_remap = params->xcd_remap < 0 ? 0 : 1;
   {
     const MoveP mp = host_move_params(params->velocity, params->width, params->height);
     kp.vel_f = mp.vel_f;
@@ -3115,10 +3107,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     MEV_HIP(hipMemset(c->rate_full, 0, sizeof(double)));
     if (n > 0) MEV_HIP(hipMemcpy(c->rate_full, tab, sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
   }
-  {
-    const char* sw = getenv("MEV_SCN");  // dev A/B switch: 0 = always the generic rollout kernel
-    c->scn_allowed = !(sw && atoi(sw) == 0);
-  }
+  c->scn_allowed = params->scenario_constants >= 0;
 
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
   c->kp.tab_m = 0;

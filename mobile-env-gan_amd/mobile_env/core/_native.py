@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -49,6 +49,8 @@ class MevParams(C.Structure):
         ("bs_class", C.c_void_p), ("ue_class", C.c_void_p),
         ("bs_class_params", C.c_void_p), ("ue_class_params", C.c_void_p),
         ("rate_table_offsets", C.c_void_p),
+        ("lds_tables", C.c_int32), ("two_groups", C.c_int32), ("stage_rows", C.c_int32),
+        ("xcd_remap", C.c_int32), ("scenario_constants", C.c_int32),
     ]
 
 

@@ -56,6 +56,12 @@ class EngineParams:
     draw_table: int = -1   # mev_params.draw_table: episode draw table pairs per env (-1 auto)
     fuse_steps: int = 0    # mev_params.fuse_steps: 0 step(n > 1) in one launch, -1 n launches
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
+    # launch-shape overrides (mev_params; 0 = automatic, results identical for every setting):
+    lds_tables: int = 0          # -1 L2 association map, 1..3 that LDS table mode
+    two_groups: int = 0          # -1 one env group per wavefront in rollouts
+    stage_rows: int = 0          # > 0: at most that many staged per-env rows per window
+    xcd_remap: int = 0           # -1 blocks in dispatch order
+    scenario_constants: int = 0  # -1 generic kernel instances only
     # heterogeneous entities (entities.py:7-22,33-45): parameter classes and each station's /
     # UE's class (None: every entity has bs / ue / velocity above); see lowering.lower
     bs_classes: "list | None" = None   # [{bw, freq, tx, height}]
@@ -133,7 +139,10 @@ class EngineParams:
             ue_height=float(self.ue["height"]),
             util_lower=float(self.util_lower), util_upper=float(self.util_upper),
             util_w1=float(self.util_coeffs[0]), util_w2=float(self.util_coeffs[1]),
-            util_w3=float(self.util_coeffs[2]), qoe_low=float(self.qoe_low))
+            util_w3=float(self.util_coeffs[2]), qoe_low=float(self.qoe_low),
+            lds_tables=int(self.lds_tables), two_groups=int(self.two_groups),
+            stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
+            scenario_constants=int(self.scenario_constants))
         cp._keep = keep
         return cp
 

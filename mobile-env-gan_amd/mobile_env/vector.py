@@ -56,7 +56,10 @@ def _bs_layouts(spec, num_envs, seeds, device):
 class VectorMobileEnv:
     def __init__(self, env_id: str, num_envs: int = 1, device=None, seed: int = 2024,
                  config: Optional[dict] = None, metrics: bool = False, rate64: bool = False,
-                 util64: bool = False, stream_split: int = 0, fuse_steps: int = 0):
+                 util64: bool = False, stream_split: int = 0, fuse_steps: int = 0,
+                 **launch):
+        """launch: EngineParams launch-shape overrides (lds_tables, two_groups, stage_rows,
+        xcd_remap, scenario_constants; default 0 = automatic)."""
         spec = registry.spec(env_id)
         cfg = deep_dict_merge(default_config(), config or {})
         if spec["velocity"] is not None:
@@ -79,7 +82,7 @@ class VectorMobileEnv:
             ue={k: cfg["ue"][k] for k in ("snr_tr", "noise", "height")},
             util_lower=cfg["utility_params"]["lower"], util_upper=cfg["utility_params"]["upper"],
             util_coeffs=tuple(cfg["utility_params"]["coeffs"]),
-            stream_split=stream_split, fuse_steps=fuse_steps)
+            stream_split=stream_split, fuse_steps=fuse_steps, **launch)
         self.engine = StepEngine(p, bs_xy, self.seeds.numpy(), bs_count=bs_count, device=device,
                                  metrics=metrics, rate64=rate64, util64=util64)
         U = self.num_ues
