@@ -33,8 +33,9 @@ Contract (see DESIGN.md "Measurement"):
   rocprofv3 PMC summary (profiles/pmc_traffic.json; FETCH_SIZE x 2 + WRITE_SIZE per the MI355X
   guide), else null.
 * roofline_step: the one-step launch of ``make().step()`` (mev_step(1)), timed after the timed
-  region (200 launches, HIP events around each), on SURVEY.md 8d's canonical bytes per
-  env-step x E -- the canonical unit of work at its canonical byte count.
+  region (200 back-to-back launches in 10 groups, HIP events around each group), on SURVEY.md
+  8d's canonical bytes per env-step x E -- the canonical unit of work at its canonical byte
+  count.
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
   per core of the host share, run before the GPU is touched.
@@ -313,18 +314,26 @@ def main():
 
     step_roof = None
     if rank == 0 and fused and not args.profile_run and args.step_launches > 0:
-        # the Gym step() launch (mev_step(1)), canonical bytes, timed after the timed region
-        evs = [(_Ev(), _Ev()) for _ in range(args.step_launches)]
+        # the Gym step() launch (mev_step(1)), canonical bytes, timed after the timed region:
+        # back-to-back launches between one event pair (an event pair around every launch
+        # adds ~2 us of marker overhead to a 19 us kernel), in 10 groups for the spread
+        step1 = eng.launcher(1)
+        for _ in range(20):
+            step1()
+        ngrp = 10
+        per = max(1, args.step_launches // ngrp)
+        evs = [(_Ev(), _Ev()) for _ in range(ngrp)]
         for a, b in evs:
             a.record()
-            eng.step(1)
+            for _ in range(per):
+                step1()
             b.record()
         torch.cuda.synchronize(device)
-        ms = sorted(a.e.elapsed_time(b.e) for a, b in evs)
+        ms = sorted(a.e.elapsed_time(b.e) / per for a, b in evs)
         avg = sum(ms) / len(ms)
         tr1, rp1 = load_profile(args.workload, E, "single")
         step_roof = roofline(E * algorithmic_bytes_per_env_step(U, per_env_bs, B), avg, tr1)
-        step_roof.update({"median_launch_ms": ms[len(ms) // 2], "launches": len(ms),
+        step_roof.update({"median_launch_ms": ms[len(ms) // 2], "launches": per * ngrp,
                           "rocprof_launch_ms": rp1,
                           "env_steps_per_s": E / (avg * 1e-3),
                           "basis": "SURVEY.md 8d canonical bytes per env-step x E, one-step "

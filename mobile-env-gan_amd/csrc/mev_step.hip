@@ -1151,7 +1151,7 @@ __device__ __forceinline__ int block_slot(int remap) {
 
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
 // Groups [g0, ngroups) of the batch (g0 > 0: second half of the two-stream shape).
-template <bool PER_ENV_BS, bool LEAN, int UC>
+template <bool PER_ENV_BS, bool LEAN, int UC, int SCN = 0>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb, int g0, int ngroups) {
   extern __shared__ int lds_hist[];  // [waves][G][B] when KPS(hist_lds)
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const bool env_ok = (m.seg < G) && (e < kp.E);
   if (g < ngroups) {
     GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
-    packed_group<PER_ENV_BS, LEAN, UC, false, 0, 0, STG>(
+    packed_group<PER_ENV_BS, LEAN, UC, false, 0, SCN, STG>(
         kp, st, out, tb, m, a, e, env_ok, lds_hist + (threadIdx.x >> 6) * G * kp.B, nullptr,
         nullptr, 0, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
         sdn + (threadIdx.x >> 6) * GC);
@@ -3320,7 +3320,11 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   const KParams& kp = c->kp;
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
-  const StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
+  StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
+  if (lean && !c->p.bs_per_env && kp.U == 30 && match_scn(c) == 2)  // scenario constants
+    k = k_step_packed<false, true, 30, 2>;
+  else if (lean && !c->p.bs_per_env && kp.U == 15 && match_scn(c) == 1)
+    k = k_step_packed<false, true, 15, 1>;
   const size_t shmem =
       kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;
   // n > 1 steps on one stream: one launch of the fused multi-step kernel
