@@ -1931,6 +1931,15 @@ __host__ __device__ inline size_t block_r100_off(int B, int M) {
 __host__ __device__ inline size_t block_lds_bytes(int B, int M) {
   return block_r100_off(B, M) + 8 * (size_t)(kMaxU + 1);
 }
+// Station culling of the scenario instance (k_steps_block CULL): the map in 4 x 4 cells, per
+// cell a 16-byte record {count, up to 15 candidate station indices}, after the other areas
+constexpr int kCullLog = 2;
+__host__ __device__ constexpr int block_cull_cells(int W, int H) {
+  return ((W + (1 << kCullLog) - 1) >> kCullLog) * ((H + (1 << kCullLog) - 1) >> kCullLog);
+}
+__host__ __device__ inline size_t block_cull_bytes(int W, int H) {
+  return 16 * (size_t)block_cull_cells(W, H);
+}
 
 __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   BlockLds l;
@@ -2047,6 +2056,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int M = KPS(tab_m);
   const BlockLds L = block_lds(lds_raw, lds_keys, KPS(B), KPS(tab_m));
   for (int n = u; n <= U; n += blockDim.x) L.r100[n] = n ? 100.0 / (double)n : 0.0;
+  // station culling (the scenario instance): per 4 x 4 cell of the map, the stations that can
+  // be the closest to some point of the cell (see the prologue)
+  constexpr bool CULL = SCN == 4 && !HET;
+  constexpr int CNX = (scn_const(SCN).W + (1 << kCullLog) - 1) >> kCullLog;
+  constexpr int CNC = CULL ? block_cull_cells(scn_const(SCN).W, scn_const(SCN).H) : 1;
+  unsigned char* const crec =
+      reinterpret_cast<unsigned char*>(lds_raw + block_lds_bytes(KPS(B), KPS(tab_m)));
   // heterogeneous entities: this UE's class and movement parameters
   const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
   const MoveP mp = HET ? tb.mv[cu]
@@ -2097,9 +2113,52 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                     (unsigned)i));
     }
     for (int i = u; i < KPS(B); i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
+    if (CULL && u == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
     bool s_ok = true;  // the slot holds the state after the env's last draw
     BlockRow prev{0, 0, 0};
     __syncthreads();
+    const bool cull = CULL && scaled && nb > 0;  // (uniform)
+    if (cull) {
+      // Candidates of cell C = [x0, x1] x [y0, y1]: s* = the station closest to a point of C,
+      // D2 = its squared distance to C's farthest corner (every point of C has a station
+      // within D2), and every station s whose squared distance to C is <= D2. A station
+      // outside the list is farther than D2 from every point of C, so strictly farther than
+      // s*: the minimum key over the list (ties by index included) is the minimum over all
+      // stations. More than 15 candidates: count 255, the lane scans every station.
+      const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
+      for (int c = u; c < CNC; c += blockDim.x) {
+        const int cy = c / CNX, cx = c - cy * CNX;
+        const int x0 = cx << kCullLog, y0 = cy << kCullLog;
+        const int x1 = min(x0 + (1 << kCullLog) - 1, KPS(W) - 1);
+        const int y1 = min(y0 + (1 << kCullLog) - 1, KPS(H) - 1);
+        const unsigned bk =
+            scan_key_pairs(kk2, 0, nb >> 1, true, make_int2(min(x0 + 2, x1), min(y0 + 2, y1)));
+        unsigned best = bk;
+        if (nb & 1) {
+          const int2 kv = lds_keys[nb - 1];
+          const s16x2 p32 = {(short)(min(x0 + 2, x1) << 5), (short)(min(y0 + 2, y1) << 5)};
+          best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
+        }
+        const int2 ks = lds_keys[best & ((1u << kKeyBits) - 1)];
+        const int sx = -(int)(short)(ks.x & 0xffff) >> 6, sy = -(int)(short)(ks.x >> 16) >> 6;
+        const int fx = max(sx - x0, x1 - sx), fy = max(sy - y0, y1 - sy);
+        const int D2 = fx * fx + fy * fy;
+        unsigned char* r = crec + 16 * c;
+        int n = 0;
+        for (int j = 0; j < nb; ++j) {
+          const int2 kv = lds_keys[j];
+          const int qx = -(int)(short)(kv.x & 0xffff) >> 6, qy = -(int)(short)(kv.x >> 16) >> 6;
+          const int dx = max(max(x0 - qx, qx - x1), 0), dy = max(max(y0 - qy, qy - y1), 0);
+          if (dx * dx + dy * dy <= D2) {
+            if (n < 15) r[1 + n] = (unsigned char)j;
+            ++n;
+          }
+        }
+        for (int j = n; j < 15; ++j) r[1 + j] = (unsigned char)nb;
+        r[0] = (unsigned char)(n > 15 ? 255 : n);
+      }
+      __syncthreads();
+    }
 
     for (int i = 0; i < nsteps; ++i) {
       const int row = traj ? i : 0;
@@ -2194,8 +2253,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       unsigned best = UINT_MAX;
       int srv = -1, d2s = 0;
       double full = 0.0;
+      // the cell's candidate list (CULL): its count and up to 15 station indices, one key per
+      // candidate (a per-lane ds_read_b64), until no lane of the wave has more
+      bool full_scan = true;
+      if (cull) {
+        const int cell = min((max(pos.y, 0) >> kCullLog) * CNX + (max(pos.x, 0) >> kCullLog), CNC - 1);
+        const v4u32 rec = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
+        const int cn = active ? (int)(rec.x & 255u) : 0;
+        full_scan = bal(cn > 15) != 0;
+        if (!full_scan) {
+          const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
+#pragma unroll
+          for (int j = 0; j < 15; ++j) {
+            if (!bal(cn > j)) break;
+            const unsigned wd = j < 3 ? rec.x : j < 7 ? rec.y : j < 11 ? rec.z : rec.w;
+            const unsigned id = __builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u);
+            const int2 kv = lds_keys[id];
+            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
+          }
+          if (!active) best = UINT_MAX;
+        }
+      }
       if (!HET) {
-        if (active) {
+        if (active && full_scan) {
           best = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos);
           if (nb & 1) {  // the odd last station
             const int2 kv = lds_keys[nb - 1];
@@ -3428,10 +3508,12 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                         : (lean ? k_steps_block<false, true, true> : k_steps_block<false, false, true>))
              : (per_env ? (lean ? k_steps_block<true, true, false> : k_steps_block<true, false, false>)
                         : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
-  if (lean && per_env && !kp.het && match_scn(c) == 4)  // mobile-custom-128x1024's constants
+  size_t shm = block_lds_bytes(kp.B, kp.tab_m);
+  if (lean && per_env && !kp.het && match_scn(c) == 4) {  // mobile-custom-128x1024's constants
     kf = k_steps_block<true, true, false, 4>;
+    shm += block_cull_bytes(kp.W, kp.H);  // its station culling records
+  }
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
-  const size_t shm = block_lds_bytes(kp.B, kp.tab_m);
   if (c->fuse_steps || nsteps == 1) {
     kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, ko, tb, nsteps, traj ? 1 : 0);
   } else {
