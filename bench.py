@@ -114,17 +114,23 @@ def max_over_ranks(value: float, device=None) -> float:
 # CPU baseline: the per-object port of the reference step, one process per core
 # ---------------------------------------------------------------------------------------------
 def _cpu_worker(args):
-    layout, num_ues, seed0, budget_s = args
+    layout, num_bs, num_ues, velocity, seed0, budget_s = args
+    import numpy as np
     from oracle import port
     done = 0
     k = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        core = port.build(layout, num_ues, seed0 + k, 1.5)
+        # per-env-layout workloads: a uniform integer layout per episode (vector._bs_layouts)
+        lay = layout if layout is not None else \
+            np.random.default_rng(seed0 + k).integers(0, 200, size=(num_bs, 2)).tolist()
+        core = port.build(lay, num_ues, seed0 + k, velocity)
         core.reset()
-        for _ in range(20):
+        for _ in range(20):  # an episode, or as much of it as the budget allows
             core.step()
             done += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
         k += 1
     return done, time.perf_counter() - t0
 
@@ -142,21 +148,26 @@ def host_share_cores() -> int:
     return max(1, n)
 
 
-def cpu_baseline(budget_s: float, procs: int):
-    from mobile_env.scenarios.registry import LAYOUTS
-    lay = LAYOUTS["large"]
+def cpu_baseline(budget_s: float, procs: int, workload: str = "mobile-large-central-v0"):
+    """The per-object port of the reference step on `workload`'s sizes (registered ids; the
+    default velocity 1.5 of MComCore.default_config where the scenario sets none)."""
+    from mobile_env.scenarios import registry
+    sp = registry.spec(workload)
+    lay = registry.LAYOUTS[sp["layout"]]["bs"] if not sp["per_env_layout"] else None
+    U, B = sp["num_ues"], sp["num_bs"]
+    vel = sp["velocity"] if sp["velocity"] is not None else 1.5
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(lay["bs"], lay["num_ues"], 1000 + 100000 * i, budget_s)
+        res = pool.map(_cpu_worker, [(lay, B, U, vel, 1000 + 100000 * i, budget_s)
                                      for i in range(procs)])
     wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
             "host_cpus": os.cpu_count(),
             "sample": (f"oracle/port.py per-object restatement of MComCore.step, "
-                       f"mobile-large-central-v0 (13 BS x 30 UE), {procs} processes (one per "
-                       f"core of the host share) x {budget_s:.0f} s of whole 20-step episodes, "
+                       f"{workload} ({B} BS x {U} UE), {procs} processes (one per "
+                       f"core of the host share) x {budget_s:.0f} s of 20-step episodes, "
                        f"seeds 1000+, compute-only (no JSON dump): {steps} env-steps in "
                        f"{wall:.1f} s")}
 
@@ -222,7 +233,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.profile_run):
-        cpu = cpu_baseline(args.cpu_budget, host_share_cores())
+        cpu = cpu_baseline(args.cpu_budget, host_share_cores(), args.workload)
 
     import torch
     import torch.distributed as dist

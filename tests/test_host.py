@@ -221,6 +221,24 @@ def test_bench_byte_models():
             assert r <= n * bench.algorithmic_bytes_per_env_step(U, False, 3)
 
 
+def test_bench_cpu_baseline_follows_workload():
+    """bench.py's cpu_baseline runs the CPU port on the --workload's sizes (shared and per-env
+    layouts), one short sample per workload."""
+    import importlib.util
+    import os
+    import sys
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    sys.modules["bench"] = bench  # (the worker function is pickled by module name)
+    spec.loader.exec_module(bench)
+    for wl, sizes in (("mobile-small-central-v0", "3 BS x 5 UE"),
+                      ("mobile-large-perenv-v0", "13 BS x 30 UE")):
+        r = bench.cpu_baseline(0.3, 1, wl)
+        assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
+        assert wl in r["sample"] and sizes in r["sample"]
+
+
 def test_sums_of_two_squares_rank_index():
     """The LDS tables index the float64 rates by the rank of d2 in S = {a^2 + b^2 <= d2max}
     (mev_step.hip build_lds_tables / k_lds_map): every squared integer distance is in S, and
