@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 11
+#define MEV_ABI_VERSION 12
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -129,8 +129,10 @@ typedef struct mev_params {
    *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
    *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges);
    *   scenario_constants: -1: the generic kernel instances only (else a registered scenario's
-   *     parameters are compiled in when every value matches). */
-  int32_t lds_tables, two_groups, stage_rows, xcd_remap, scenario_constants;
+   *     parameters are compiled in when every value matches);
+   *   station_culling: -1: the U > 64 kernel scans every station per UE (else per-cell
+   *     candidate lists where the layout qualifies: 32..255 stations, map <= 512 x 512). */
+  int32_t lds_tables, two_groups, stage_rows, xcd_remap, scenario_constants, station_culling;
 } mev_params;
 
 typedef struct mev_state {

@@ -87,6 +87,9 @@ struct KParams {
   int lbs;            // fused per-env-layout launches: station slots per env staged in LDS (0: off)
   int het;            // heterogeneous entities: nb_cls station classes, nu_cls UE classes
   int nb_cls, nu_cls, bperm;
+  // block kernel station culling (0: off): cells of 2^cull_log x 2^cull_log, cull_nx per row,
+  // cull_nc in all (block_cull_params)
+  int cull_log, cull_nx, cull_nc;
 };
 
 struct KState {
@@ -239,6 +242,7 @@ struct ScnConst {
   unsigned vel_f, move_lim, inv_w, inv_h, u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale,
       u_offset;
   int d2max;
+  int cull_log, cull_nx, cull_nc;
 };
 __host__ __device__ constexpr ScnConst scn_const(int scn) {
 #define MEV_SCN_F32 2, 1, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
@@ -258,7 +262,7 @@ __host__ __device__ constexpr ScnConst scn_const(int scn) {
        : scn == 4 ? ScnConst{1024, 128, 200, 200, 3080, 0, 20, 0, 20, 1, 0, 0, 0, 0, 100, 1,
                              0x41200000u, 0x3effec00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u,
                              0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u,
-                             19362}
+                             19362, 2, 50, 2500}
                   : ScnConst{};
 }
 #define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
@@ -1931,14 +1935,28 @@ __host__ __device__ inline size_t block_r100_off(int B, int M) {
 __host__ __device__ inline size_t block_lds_bytes(int B, int M) {
   return block_r100_off(B, M) + 8 * (size_t)(kMaxU + 1);
 }
-// Station culling of the scenario instance (k_steps_block CULL): the map in 4 x 4 cells, per
-// cell a 16-byte record {count, up to 15 candidate station indices}, after the other areas
-constexpr int kCullLog = 2;
-__host__ __device__ constexpr int block_cull_cells(int W, int H) {
-  return ((W + (1 << kCullLog) - 1) >> kCullLog) * ((H + (1 << kCullLog) - 1) >> kCullLog);
-}
-__host__ __device__ inline size_t block_cull_bytes(int W, int H) {
-  return 16 * (size_t)block_cull_cells(W, H);
+// Station culling (k_steps_block): the map in square cells of 2^cull_log, per cell a 16-byte
+// LDS record {count, up to 15 candidate station indices} after the other areas. Chosen on the
+// host for homogeneous layouts of 32..255 stations on maps up to 512 x 512: the cell side about
+// a third of the mean station spacing sqrt(W H / B), doubled until the records fit 40 KB (the
+// block kernel's two workgroups per CU); 128 stations on 200 x 200: 4 x 4 cells, 2,500 records,
+// 1.8 candidates per cell on average.
+struct CullP {
+  int log, nx, nc;
+};
+inline CullP block_cull_params(int B, int W, int H, bool het) {
+  CullP r{0, 0, 0};
+  if (het || B < 32 || B > 255 || W > 512 || H > 512) return r;
+  const double spacing = sqrt((double)W * (double)H / (double)B);
+  int k = 1;
+  while ((double)(2 << k) <= spacing / 3.0) ++k;
+  for (;; ++k) {
+    const int nx = (W + (1 << k) - 1) >> k, ny = (H + (1 << k) - 1) >> k;
+    if (16 * nx * ny <= 40960) {
+      r = CullP{k, nx, nx * ny};
+      return r;
+    }
+  }
 }
 
 __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
@@ -2056,11 +2074,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int M = KPS(tab_m);
   const BlockLds L = block_lds(lds_raw, lds_keys, KPS(B), KPS(tab_m));
   for (int n = u; n <= U; n += blockDim.x) L.r100[n] = n ? 100.0 / (double)n : 0.0;
-  // station culling (the scenario instance): per 4 x 4 cell of the map, the stations that can
-  // be the closest to some point of the cell (see the prologue)
-  constexpr bool CULL = SCN == 4 && !HET;
-  constexpr int CNX = (scn_const(SCN).W + (1 << kCullLog) - 1) >> kCullLog;
-  constexpr int CNC = CULL ? block_cull_cells(scn_const(SCN).W, scn_const(SCN).H) : 1;
+  // station culling: per cell of the map, the stations that can be the closest to some point
+  // of the cell (see the prologue)
+  const bool CULL = !HET && KPS(cull_log) > 0;
+  const int CLOG = KPS(cull_log), CNX = KPS(cull_nx), CNC = KPS(cull_nc);
   unsigned char* const crec =
       reinterpret_cast<unsigned char*>(lds_raw + block_lds_bytes(KPS(B), KPS(tab_m)));
   // heterogeneous entities: this UE's class and movement parameters
@@ -2117,7 +2134,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     bool s_ok = true;  // the slot holds the state after the env's last draw
     BlockRow prev{0, 0, 0};
     __syncthreads();
-    const bool cull = CULL && scaled && nb > 0;  // (uniform)
+    // (uniform; launches of >= 32 steps: the records cost about as much as 18 steps' full scans)
+    const bool cull = CULL && scaled && nb > 0 && nsteps >= 32;
     if (cull) {
       // Candidates of cell C = [x0, x1] x [y0, y1]: s* = the station closest to a point of C,
       // D2 = its squared distance to C's farthest corner (every point of C has a station
@@ -2128,15 +2146,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
       for (int c = u; c < CNC; c += blockDim.x) {
         const int cy = c / CNX, cx = c - cy * CNX;
-        const int x0 = cx << kCullLog, y0 = cy << kCullLog;
-        const int x1 = min(x0 + (1 << kCullLog) - 1, KPS(W) - 1);
-        const int y1 = min(y0 + (1 << kCullLog) - 1, KPS(H) - 1);
-        const unsigned bk =
-            scan_key_pairs(kk2, 0, nb >> 1, true, make_int2(min(x0 + 2, x1), min(y0 + 2, y1)));
+        const int x0 = cx << CLOG, y0 = cy << CLOG;
+        const int x1 = min(x0 + (1 << CLOG) - 1, KPS(W) - 1);
+        const int y1 = min(y0 + (1 << CLOG) - 1, KPS(H) - 1);
+        const int xm = (x0 + x1) >> 1, ym = (y0 + y1) >> 1;  // a point of the cell
+        const unsigned bk = scan_key_pairs(kk2, 0, nb >> 1, true, make_int2(xm, ym));
         unsigned best = bk;
         if (nb & 1) {
           const int2 kv = lds_keys[nb - 1];
-          const s16x2 p32 = {(short)(min(x0 + 2, x1) << 5), (short)(min(y0 + 2, y1) << 5)};
+          const s16x2 p32 = {(short)(xm << 5), (short)(ym << 5)};
           best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
         }
         const int2 ks = lds_keys[best & ((1u << kKeyBits) - 1)];
@@ -2257,7 +2275,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // candidate (a per-lane ds_read_b64), until no lane of the wave has more
       bool full_scan = true;
       if (cull) {
-        const int cell = min((max(pos.y, 0) >> kCullLog) * CNX + (max(pos.x, 0) >> kCullLog), CNC - 1);
+        const int cell = min((max(pos.y, 0) >> CLOG) * CNX + (max(pos.x, 0) >> CLOG), CNC - 1);
         const v4u32 rec = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
         const int cn = active ? (int)(rec.x & 255u) : 0;
         full_scan = bal(cn > 15) != 0;
@@ -2311,11 +2329,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
         if (lane == 0) L.wt[32 + w] = nc;
       }
-      // the rate gather is waited for here, on every path, before this step's stores: a lane or
-      // wave that never reads `full` would carry the load as pending to a later merge, whose
-      // vmcnt(0) (before the register is reused) would then also wait for the stores
-      asm volatile("" ::"v"(full));
       __syncthreads();  // ---- barrier 2
+      // the rate gather is waited for here (after the barrier: its latency overlaps the wait for
+      // the other waves), on every path, before this step's stores: a lane or wave that never
+      // reads `full` would carry the load as pending to a later merge, whose vmcnt(0) (before
+      // the register is reused) would then also wait for the stores
+      asm volatile("" ::"v"(full));
 
       // ---- C: ResourceFair share + rounding, utility, stores, partial sums -------------
       double cents = 0.0;
@@ -2719,7 +2738,8 @@ static int match_scn(const mev_ctx* ctx) {
         fbits(kp.inv_w) == c.inv_w && fbits(kp.inv_h) == c.inv_h &&
         fbits(kp.u_log2_coef) == c.u_log2_coef && fbits(kp.u_w2f) == c.u_w2f &&
         fbits(kp.u_lowerf) == c.u_lowerf && fbits(kp.u_upperf) == c.u_upperf &&
-        fbits(kp.u_scale) == c.u_scale && fbits(kp.u_offset) == c.u_offset)
+        fbits(kp.u_scale) == c.u_scale && fbits(kp.u_offset) == c.u_offset &&
+        kp.cull_log == c.cull_log && kp.cull_nx == c.cull_nx && kp.cull_nc == c.cull_nc)
       return s;
   }
   return 0;
@@ -3047,6 +3067,7 @@ static int build_het(mev_ctx* c) {
   }
   seg[NB] = (int)perm.size();
   kp.het = 1;
+  kp.cull_log = kp.cull_nx = kp.cull_nc = 0;  // (class segments: no culling)
   kp.nb_cls = NB;
   kp.nu_cls = NU;
   kp.bperm = (int)perm.size();
@@ -3135,6 +3156,13 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
   kp.xcd_remap = params->xcd_remap < 0 ? 0 : 1;
+  if (params->num_ues > 64 && params->station_culling >= 0) {  // block kernel (block_cull_params)
+    const CullP cp = block_cull_params(params->num_bs, params->width, params->height,
+                                       false);
+    kp.cull_log = cp.log;
+    kp.cull_nx = cp.nx;
+    kp.cull_nc = cp.nc;
+  }
   {
     const MoveP mp = host_move_params(params->velocity, params->width, params->height);
     kp.vel_f = mp.vel_f;
@@ -3508,11 +3536,9 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                         : (lean ? k_steps_block<false, true, true> : k_steps_block<false, false, true>))
              : (per_env ? (lean ? k_steps_block<true, true, false> : k_steps_block<true, false, false>)
                         : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
-  size_t shm = block_lds_bytes(kp.B, kp.tab_m);
-  if (lean && per_env && !kp.het && match_scn(c) == 4) {  // mobile-custom-128x1024's constants
+  const size_t shm = block_lds_bytes(kp.B, kp.tab_m) + 16 * (size_t)kp.cull_nc;  // (culling records)
+  if (lean && per_env && !kp.het && match_scn(c) == 4)  // mobile-custom-128x1024's constants
     kf = k_steps_block<true, true, false, 4>;
-    shm += block_cull_bytes(kp.W, kp.H);  // its station culling records
-  }
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
   if (c->fuse_steps || nsteps == 1) {
     kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, ko, tb, nsteps, traj ? 1 : 0);

@@ -62,6 +62,7 @@ class EngineParams:
     stage_rows: int = 0          # > 0: at most that many staged per-env rows per window
     xcd_remap: int = 0           # -1 blocks in dispatch order
     scenario_constants: int = 0  # -1 generic kernel instances only
+    station_culling: int = 0     # -1 U > 64: scan every station (no per-cell candidate lists)
     # heterogeneous entities (entities.py:7-22,33-45): parameter classes and each station's /
     # UE's class (None: every entity has bs / ue / velocity above); see lowering.lower
     bs_classes: "list | None" = None   # [{bw, freq, tx, height}]
@@ -142,7 +143,8 @@ class EngineParams:
             util_w3=float(self.util_coeffs[2]), qoe_low=float(self.qoe_low),
             lds_tables=int(self.lds_tables), two_groups=int(self.two_groups),
             stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
-            scenario_constants=int(self.scenario_constants))
+            scenario_constants=int(self.scenario_constants),
+            station_culling=int(self.station_culling))
         cp._keep = keep
         return cp
 
