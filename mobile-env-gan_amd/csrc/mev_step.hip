@@ -1564,7 +1564,11 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
           best = min(best, min(k0, k1));
         }
       };
-      if (KPS(B) <= 8) scan(std::integral_constant<int, 4>());
+      // (scenario constants: ceil(B / 2) slot pairs -- the slots past the env's stations hold
+      // the never-winning key)
+      constexpr int NPS = SCN ? (scn_const(SCN).B + 1) / 2 : 0;
+      if (NPS) scan(std::integral_constant<int, NPS ? NPS : 1>());
+      else if (KPS(B) <= 8) scan(std::integral_constant<int, 4>());
       else scan(std::integral_constant<int, 8>());
       const int d2s = (int)(best >> 4) - (1 << 21) + __mul24(c[r].pos.x, c[r].pos.x) +
                       __mul24(c[r].pos.y, c[r].pos.y);
