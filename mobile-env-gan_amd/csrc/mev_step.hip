@@ -316,8 +316,35 @@ __device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) 
 }
 
 // The context's movement parameters (compile-time constants in a scenario instance).
+// Velocity 1.5 (the registered scenarios' constants) in integers, exactly: off the axes
+// |q| = 1.5 |dx| / |v| lies strictly between 0 and 1.5, and |q| > 1/2 <=> 8 dx^2 > dy^2
+// (equality has no integer solution but 0, and |q| stays > 1e-7 away from 1/2 for coordinates
+// < 1024, far beyond float64's rounding of the reference's expression), so the step is
+// sgn(dx) [8 dx^2 > dy^2]; on an axis q = +-1.5 exactly, and np.round's half-to-even gives
+// |step| 2 from an even coordinate, 1 from an odd one. (Arrival, d2 <= 2, is the caller's;
+// tests/test_oracle.py checks the formula against the reference expression for every
+// displacement of a 200 x 200 map.)
+__device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int ay2) {
+  const int sx = (ax2 << 3 > ay2 ? 1 : 0) + (dy == 0 && !(pos.x & 1) ? 1 : 0);
+  const int sy = (ay2 << 3 > ax2 ? 1 : 0) + (dx == 0 && !(pos.y & 1) ? 1 : 0);
+  return make_int2(pos.x + (dx < 0 ? -sx : sx), pos.y + (dy < 0 ? -sy : sy));
+}
+template <int SCN>
+constexpr bool scn_v15() { return SCN != 0 && scn_const(SCN).vel_f == 0x3fc00000u; }
+
 template <int SCN = 0>
 __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
+  if constexpr (scn_v15<SCN>()) {
+    const int dx = wp.x - pos.x, dy = wp.y - pos.y;
+    const int ax2 = __mul24(dx, dx), ay2 = __mul24(dy, dy);
+    if (ax2 + ay2 <= 2) {  // arrived (sqrt(d2) <= 1.5): snap to the waypoint and pop it
+      pos = wp;
+      wp = make_int2(-1, -1);
+    } else {
+      pos = step_v15(pos, dx, dy, ax2, ay2);
+    }
+    return;
+  }
   move_ue_p(pos, wp, MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)});
 }
 
@@ -1509,14 +1536,20 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   // (move_ue_p per lane: arrival snap; axis-parallel moves exactly in float32 when the velocity
   // is a float32 value (scenario constants); the float32 step clear of a tie; else float64)
   constexpr bool AXF = SCN != 0;  // scenario velocity 1.5: pos +- 1.5 exact in float32
+  constexpr bool V15 = scn_v15<SCN>();  // velocity 1.5 in integers (step_v15)
   int2 npos[R];
   bool arrive[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int2 pos = c[r].pos, wp = c[r].wp;
     const int dx = wp.x - pos.x, dy = wp.y - pos.y;
-    const int d2 = __mul24(dx, dx) + __mul24(dy, dy);
+    const int ax2 = __mul24(dx, dx), ay2 = __mul24(dy, dy);
+    const int d2 = ax2 + ay2;
     arrive[r] = d2 <= KPS(d2snap);
+    if constexpr (V15) {
+      npos[r] = arrive[r] ? wp : step_v15(pos, dx, dy, ax2, ay2);
+      continue;
+    }
     const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);
     const float qx = (float)dx * sc, qy = (float)dy * sc;
     const float rx = rintf(qx), ry = rintf(qy);

@@ -178,3 +178,36 @@ def test_vec_oracle_matches_heterogeneous_fixture():
         act = ~np.isnan(d["util"][:, s])
         np.testing.assert_array_equal(o["util"][act], d["util"][:, s][act])
         np.testing.assert_array_equal(o["metrics"][:, :3], d["metrics"][:, s, :3])
+
+
+def test_velocity_15_integer_step_matches_reference_expression():
+    """The kernels' integer movement at velocity 1.5 (step_v15 in mev_step.hip: arrival at
+    d2 <= 2; else per axis sgn(dx) [8 dx^2 > dy^2], and on an axis |step| 2 from an even
+    coordinate, 1 from an odd one) equals movement.py:49-62's float64 expression
+    np.round(position + velocity * v / norm(v)) for every displacement on a 200 x 200 map, at
+    positions of both parities and at the map's edges."""
+    d = np.arange(-199, 200)
+    dx, dy = (a.ravel() for a in np.meshgrid(d, d, indexing="ij"))
+    d2 = dx * dx + dy * dy
+    keep = d2 > 2
+    dx, dy, d2 = dx[keep], dy[keep], d2[keep]
+    v = np.stack([dx, dy], 1)
+    norm = np.sqrt(d2.astype(np.float64))  # == np.linalg.norm of each integer 2-vector
+    for px, py in ((0, 1), (1, 0), (100, 101), (198, 199), (199, 198)):
+        ref = np.round(np.array([px, py]) + 1.5 * v / norm[:, None]).astype(np.int64)
+        ax2, ay2 = dx * dx, dy * dy
+        sx = (8 * ax2 > ay2).astype(np.int64) + ((dy == 0) & (px % 2 == 0))
+        sy = (8 * ay2 > ax2).astype(np.int64) + ((dx == 0) & (py % 2 == 0))
+        got = np.stack([px + np.where(dx < 0, -sx, sx), py + np.where(dy < 0, -sy, sy)], 1)
+        np.testing.assert_array_equal(got, ref, err_msg=f"position {(px, py)}")
+    # the expression's own per-UE form (movement.py:58-60) on a sample agrees with the batch form
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        pos = rng.integers(0, 200, size=2)
+        wp = rng.integers(0, 200, size=2)
+        vv = wp - pos
+        if np.linalg.norm(vv) <= 1.5:
+            continue
+        one = np.round(pos + 1.5 * vv / np.linalg.norm(vv)).astype(int)
+        n2 = float(np.sqrt(float(vv @ vv)))
+        assert tuple(one) == tuple(np.round(pos + 1.5 * vv / n2).astype(int))
