@@ -2318,13 +2318,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         full_scan = bal(cn > 15) != 0;
         if (!full_scan) {
           const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
-#pragma unroll
-          for (int j = 0; j < 15; ++j) {
-            if (!bal(cn > j)) break;
+          // the first four candidates unconditionally (four reads in flight; past a lane's
+          // count the record holds the padding index, whose key never wins), then one at a
+          // time while a lane of the wave has more
+          auto key_of = [&](int j) {
             const unsigned wd = j < 3 ? rec.x : j < 7 ? rec.y : j < 11 ? rec.z : rec.w;
-            const unsigned id = __builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u);
-            const int2 kv = lds_keys[id];
-            best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
+            const int2 kv = lds_keys[__builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u)];
+            return (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false);
+          };
+          best = min(min(key_of(0), key_of(1)), min(key_of(2), key_of(3)));
+#pragma unroll
+          for (int j = 4; j < 15; ++j) {
+            if (!bal(cn > j)) break;
+            best = min(best, key_of(j));
           }
           if (!active) best = UINT_MAX;
         }

@@ -12,7 +12,7 @@
 # usage: tools/profile.sh TAG [bench args...]
 set -o pipefail
 TAG=${1:-r02}; shift
-ARGS="--profile-run --steps 1000 --warmup 1001 --warmup-floor-s 0 $*"
+ARGS="--profile-run --steps 1000 --warmup 1001 --warmup-floor-s 2 $*"
 RAW=/tmp/prof_$TAG
 OUT=gpurun_out/profiles
 mkdir -p $RAW $OUT
