@@ -36,9 +36,12 @@ def main():
     dev = torch.device("cuda", 0)
     score_layouts(xy[:1024], cnt[:1024], device=dev)  # warm (module load, first launches)
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    out = score_layouts(xy, cnt, device=dev)
-    e2e = time.perf_counter() - t0
+    e2e_all = []
+    for _ in range(3):  # (one-shot timings of engine build + run vary with the host: best of 3)
+        t0 = time.perf_counter()
+        out = score_layouts(xy, cnt, device=dev)
+        e2e_all.append(time.perf_counter() - t0)
+    e2e = min(e2e_all)
 
     # the episode alone: 20 fused steps on a prepared engine, QoE statistics accumulated
     p = EngineParams(num_envs=N, num_ues=7, num_bs=xy.shape[1], velocity=10.0)
@@ -60,7 +63,7 @@ def main():
     ep = min(times)
     print(json.dumps({
         "bench": "score_layouts", "layouts": N, "ues": 7, "steps_per_episode": 20,
-        "end_to_end_s": e2e, "layouts_per_s_end_to_end": N / e2e,
+        "end_to_end_s": e2e, "end_to_end_s_all": e2e_all, "layouts_per_s_end_to_end": N / e2e,
         "episode_s_best": ep, "episode_s_all": times,
         "layouts_per_s_episode": N / ep, "env_steps_per_s_episode": N * 20 / ep,
         "best_layout": int(out["best"]), "best_score": float(out["Score"][out["best"]])}))
