@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 12
+#define MEV_ABI_VERSION 13
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -203,8 +203,14 @@ int mev_share_cents(const mev_ctx* ctx, int32_t nmax, int32_t path, double* dst,
 
 /* The rollout kernel instance mev_rollout runs for this context: 0 generic, s > 0 the
  * registered scenario s compiled with its parameters as constants (chosen when every value
- * matches; MEV_SCN=0 in the environment at mev_create forces the generic instance). */
+ * matches; mev_params.scenario_constants = -1 forces the generic instance). */
 int mev_rollout_instance(const mev_ctx* ctx);
+
+/* 1 when the context's rate table needs no tie test in the LDS rollouts' ResourceFair share:
+ * for every entry and every share count n <= num_ues (<= 64), rint(full * fl(100 / n)) equals
+ * the reference's rint(fl(full / n) * 100) (checked exhaustively at mev_create); the
+ * scenario-constant two-group kernels then skip the test and its exact fallback. */
+int mev_share_tie_free(const mev_ctx* ctx);
 
 /* Host helper: numpy-compatible seeding, np.random.default_rng(seed) ->
  * SeedSequence(seed) -> PCG64 (movement seed = config seed + 4, base.py:156-168).

@@ -331,6 +331,14 @@ __device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int 
 }
 template <int SCN>
 constexpr bool scn_v15() { return SCN != 0 && scn_const(SCN).vel_f == 0x3fc00000u; }
+// Every UE active at every step (a scenario with arrival at 0, no departure before the episode
+// end, the first step active): after the lazy reset 0 <= t < t_end, so the activity test of
+// base.py:288-291 is constant -- active = valid, no compares, no ballot.
+template <int SCN>
+constexpr bool scn_all_active() {
+  return SCN != 0 && scn_const(SCN).arr_start == 0 &&
+         scn_const(SCN).arr_exit >= scn_const(SCN).t_end && scn_const(SCN).first_step_active;
+}
 
 template <int SCN = 0>
 __device__ __forceinline__ void move_ue(int2& pos, int2& wp, const KParams& kp) {
@@ -800,13 +808,16 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // activeUsers during step t: startTime <= t < exitTime (base.py:288-291, custom.py:53-54)
-  const bool active = valid && t >= KPS(arr_start) && t < KPS(arr_exit) &&
-                      (KPS(first_step_active) || t != 0);
+  const bool active = valid && (scn_all_active<SCN>() ||
+                                (t >= KPS(arr_start) && t < KPS(arr_exit) &&
+                                 (KPS(first_step_active) || t != 0)));
 
   // ---- 1. movement: lazy waypoint draws in ue_id order (movement.py:44-47) ------------
   const uint64_t act_w =
-      bal(t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0)) &
-      valid_w;
+      scn_all_active<SCN>()
+          ? valid_w
+          : bal(t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0)) &
+                valid_w;
   const bool need = active && wp.x < 0;
   const uint64_t mneed_w = bal(wp.x < 0) & act_w;
   int tot, rank;  // draws of this env this step (2 per waypoint); this lane's rank among them
@@ -1425,7 +1436,7 @@ struct Ctx2 {
   int2 pos, wp;
 };
 
-template <int UC, int SCN, int R, bool PE>
+template <int UC, int SCN, int R, bool PE, bool TF = false>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
                                           const int (&e)[R], const int (&nok)[R], int kval,
@@ -1477,9 +1488,10 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       }
     }
     const int t = c[r].t;
-    const bool on = t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0);
+    const bool on = scn_all_active<SCN>() ||
+                    (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
     active[r] = valid[r] && on;
-    act_w[r] = bal(on) & valid_w[r];
+    act_w[r] = scn_all_active<SCN>() ? valid_w[r] : bal(on) & valid_w[r];
     need[r] = active[r] && c[r].wp.x < 0;
     mneed_w[r] = bal(c[r].wp.x < 0) & act_w[r];
     const uint32_t f = seg_field<PC>(mneed_w[r], m);
@@ -1658,7 +1670,8 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     const double rr = rint(cc);
     const float d = (float)(cc - rr);
     const float rf = (float)rr;
-    tie[r] = srv[r] >= 0 && !(0.5f - fabsf(d) > __builtin_fmaf(rf, 0x1p-46f, 0x1p-25f));
+    // (TF: the host showed the product rounds like the reference for every rate and count)
+    tie[r] = !TF && srv[r] >= 0 && !(0.5f - fabsf(d) > __builtin_fmaf(rf, 0x1p-46f, 0x1p-25f));
     cf[r] = srv[r] >= 0 ? rf : 0.f;
   }
 #pragma unroll
@@ -1726,7 +1739,7 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 
 // PE: per-env station layouts (KParams::lds_mode 4: the blob holds the rank index of S, 100/n
 // and rate_full over S; the env's station keys are staged per launch like k_steps_packed's)
-template <int UC, int SCN, bool PE = false>
+template <int UC, int SCN, bool PE = false, bool TF = false>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -1826,7 +1839,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
     __builtin_amdgcn_s_waitcnt(0);
     for (int i = 0, sr = 0; i < nsteps; ++i, sr = sr + 1 == stage_rows ? 0 : sr + 1) {
-      lds2_step<UC, SCN, R, PE>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
+      lds2_step<UC, SCN, R, PE, TF>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
                                 lblob, lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
                                 drow + sr * NWG + wvu * G * R, lkeys);
       if (sr + 1 == stage_rows || i + 1 == nsteps)
@@ -2675,6 +2688,7 @@ struct mev_ctx {
   hipStream_t aux;    // second stream of the two-half shape
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
+  int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
   // heterogeneous entities (build_het)
   uint8_t* h_bcl;
   uint8_t* h_ucl;
@@ -2764,6 +2778,23 @@ static unsigned fbits(float f) {
   memcpy(&u, &f, 4);
   return u;
 }
+// True when, for every full rate of the table and every share count n <= nmax, the fast
+// product of the LDS kernels rounds like the reference: rint(full * fl(100 / n)) ==
+// rint(fl(full / n) * 100) (base.py:435, numpy round(., 2)). The rollout kernels then skip the
+// tie test and its exact fallback (k_steps_lds2 TF). Exhaustive over the table (~20k entries x
+// n), IEEE double on the host like the device's; a table that fails anywhere keeps the test.
+static bool share_tie_free(const double* full, int64_t n_d2, int nmax) {
+  if (!full || n_d2 <= 0 || nmax < 1 || nmax > 64) return false;
+  for (int n = 1; n <= nmax; ++n) {
+    const double r100 = 100.0 / (double)n;
+    for (int64_t d = 0; d < n_d2; ++d) {
+      const double f = full[d];
+      if (rint(f * r100) != rint((f / (double)n) * 100.0)) return false;
+    }
+  }
+  return true;
+}
+
 static int match_scn(const mev_ctx* ctx) {
   if (!ctx->scn_allowed) return 0;
   const KParams& kp = ctx->kp;
@@ -3257,6 +3288,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     }
     MEV_HIP(hipMemset(c->rate_full, 0, sizeof(double)));
     if (n > 0) MEV_HIP(hipMemcpy(c->rate_full, tab, sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+    c->tie_free = params->num_ues <= 64 && share_tie_free(tab, n, params->num_ues);
   }
   c->scn_allowed = params->scenario_constants >= 0;
 
@@ -3377,6 +3409,8 @@ int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EI
 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 
+int mev_share_tie_free(const mev_ctx* c) { return c ? c->tie_free : MEV_EINVAL; }
+
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
   const bool lean_ok = !c->kp.util_direct;
@@ -3491,7 +3525,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     if (c->p.bs_per_env && kp.lds_mode == 4 && lean && traj && c->lds2_wgs > 0 &&
         pairs >= c->lds2_wgs * kLds2Waves) {  // per-env layouts (k_steps_lds2<U, 0, true>)
       StepsKernel k2 = kp.U == 15 ? k_steps_lds2<15, 0, true>
-                                  : (match_scn(c) == 3 ? k_steps_lds2<30, 3, true>
+                                  : (match_scn(c) == 3 ? (c->tie_free ? k_steps_lds2<30, 3, true, true>
+                                                                      : k_steps_lds2<30, 3, true>)
                                                        : k_steps_lds2<30, 0, true>);
       const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
       const int G = kp.envs_per_wave;
@@ -3506,8 +3541,13 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     }
     if (ldsm == 3 && lean && c->lds2_wgs > 0 && pairs >= c->lds2_wgs * kLds2Waves) {
       const int scn = match_scn(c);
-      StepsKernel k2 = kp.U == 15 ? (scn == 1 ? k_steps_lds2<15, 1> : k_steps_lds2<15, 0>)
-                                  : (scn == 2 ? k_steps_lds2<30, 2> : k_steps_lds2<30, 0>);
+      const bool tf = c->tie_free != 0;  // (scenario instances only)
+      StepsKernel k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true>
+                                                    : k_steps_lds2<15, 1>)
+                                              : k_steps_lds2<15, 0>)
+                                  : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true>
+                                                    : k_steps_lds2<30, 2>)
+                                              : k_steps_lds2<30, 0>);
       const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
       const int G = kp.envs_per_wave;
       const int srows = std::min(c->stage_rows2, nsteps);

@@ -295,6 +295,11 @@ class StepEngine:
         """Rollout kernel instance: 0 generic, s > 0 registered scenario s with constants."""
         return int(self._lib.mev_rollout_instance(self._ctx))
 
+    @property
+    def share_tie_free(self) -> bool:
+        """The rate table needs no tie test in the LDS rollouts' share (mev_share_tie_free)."""
+        return bool(self._lib.mev_share_tie_free(self._ctx))
+
     def share_cents(self, nmax: int, path: int = 0):
         """Device rounded shares rint((rate_full[d2] / n) * 100) for n in [1, nmax] as the
         kernels form them (path 0: reciprocal form; 1: 100/n table form, nmax <= 64):
