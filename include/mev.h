@@ -206,10 +206,11 @@ int mev_share_cents(const mev_ctx* ctx, int32_t nmax, int32_t path, double* dst,
  * matches; mev_params.scenario_constants = -1 forces the generic instance). */
 int mev_rollout_instance(const mev_ctx* ctx);
 
-/* 1 when the context's rate table needs no tie test in the LDS rollouts' ResourceFair share:
- * for every entry and every share count n <= num_ues (<= 64), rint(full * fl(100 / n)) equals
- * the reference's rint(fl(full / n) * 100) (checked exhaustively at mev_create); the
- * scenario-constant two-group kernels then skip the test and its exact fallback. */
+/* 1 when the context's rate table needs no tie test in the ResourceFair share of the kernels
+ * that form it from a 100/n table: for every entry and every share count n <= num_ues,
+ * rint(full * fl(100 / n)) equals the reference's rint(fl(full / n) * 100) (checked
+ * exhaustively at mev_create); the scenario-constant two-group and block kernels then skip the
+ * test and its exact fallback. */
 int mev_share_tie_free(const mev_ctx* ctx);
 
 /* Host helper: numpy-compatible seeding, np.random.default_rng(seed) ->

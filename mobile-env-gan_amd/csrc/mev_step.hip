@@ -2109,7 +2109,7 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
 //   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums
 // The per-station counts alternate between two LDS arrays (the next step's array is zeroed
 // in its B phase), so two barriers per step suffice.
-template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0>
+template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0, bool TF = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
   extern __shared__ __align__(16) char lds_raw[];
@@ -2397,7 +2397,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       float cents_f = 0.f;
       if (srv >= 0) {
         const int n = cnt[srv];
-        cents = share_cents_r(full, L.r100[n], n, cents_f);
+        if (TF) {  // tie-free table (share_tie_free): the product rounds like the reference
+          cents = rint(full * L.r100[n]);
+          cents_f = (float)cents;
+        } else {
+          cents = share_cents_r(full, L.r100[n], n, cents_f);
+        }
       }
       const bool exact_util = !LEAN;
       const double rate = cents / 100.0;
@@ -2784,7 +2789,7 @@ static unsigned fbits(float f) {
 // tie test and its exact fallback (k_steps_lds2 TF). Exhaustive over the table (~20k entries x
 // n), IEEE double on the host like the device's; a table that fails anywhere keeps the test.
 static bool share_tie_free(const double* full, int64_t n_d2, int nmax) {
-  if (!full || n_d2 <= 0 || nmax < 1 || nmax > 64) return false;
+  if (!full || n_d2 <= 0 || nmax < 1 || nmax > kMaxU) return false;
   for (int n = 1; n <= nmax; ++n) {
     const double r100 = 100.0 / (double)n;
     for (int64_t d = 0; d < n_d2; ++d) {
@@ -3288,7 +3293,7 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     }
     MEV_HIP(hipMemset(c->rate_full, 0, sizeof(double)));
     if (n > 0) MEV_HIP(hipMemcpy(c->rate_full, tab, sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
-    c->tie_free = params->num_ues <= 64 && share_tie_free(tab, n, params->num_ues);
+    c->tie_free = share_tie_free(tab, n, params->num_ues);
   }
   c->scn_allowed = params->scenario_constants >= 0;
 
@@ -3621,7 +3626,7 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                         : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
   const size_t shm = block_lds_bytes(kp.B, kp.tab_m) + 16 * (size_t)kp.cull_nc;  // (culling records)
   if (lean && per_env && !kp.het && match_scn(c) == 4)  // mobile-custom-128x1024's constants
-    kf = k_steps_block<true, true, false, 4>;
+    kf = c->tie_free ? k_steps_block<true, true, false, 4, true> : k_steps_block<true, true, false, 4>;
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
   if (c->fuse_steps || nsteps == 1) {
     kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, ko, tb, nsteps, traj ? 1 : 0);

@@ -216,10 +216,10 @@ def test_velocity_15_integer_step_matches_reference_expression():
 def test_reference_channel_tables_share_tie_free(golden_dir):
     """The LDS rollouts' fast ResourceFair share rint(full * fl(100 / n)) equals the reference's
     rint(fl(full / n) * 100) (base.py:435) for every entry of both reference channel tables and
-    every share count n <= 64 -- the exhaustive condition under which mev_create selects the
-    tie-free two-group kernels (mev_share_tie_free; the GPU tests check the flag)."""
+    every share count n <= 1024 -- the exhaustive condition under which mev_create selects the
+    tie-free two-group / block kernels (mev_share_tie_free; the GPU tests check the flag)."""
     for name in ("channel_default", "channel_notebook"):
         r = np.load(f"{golden_dir}/{name}.npz")["rate"]
-        for n in range(1, 65):
+        for n in range(1, 1025):
             np.testing.assert_array_equal(np.rint(r * (100.0 / n)), np.rint((r / n) * 100.0),
                                           err_msg=f"{name} n={n}")
