@@ -725,7 +725,7 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //         (four dependent reads), 2 = station map + per-cell rank map (two parallel reads and
 //         the rate).
 template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0, int SCN = 0,
-          bool STG = false>
+          bool STG = false, bool TF = false>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
                                              const KOut& out, const KTables& tb,
                                              const LaneMap& m, GroupIn& cur, int e,
@@ -1044,10 +1044,16 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
   float cents_f = 0.f;
-  if (srv >= 0)
-    cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
-                                           lblob + KPS(lds_r100_off) + 8u * (uint32_t)n), n, cents_f)
-                 : share_cents(full, n, cents_f);
+  if (srv >= 0) {
+    if (LDSA && TF) {  // tie-free table (share_tie_free): the product rounds like the reference
+      cents = rint(full * *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n));
+      cents_f = (float)cents;
+    } else {
+      cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
+                                             lblob + KPS(lds_r100_off) + 8u * (uint32_t)n), n, cents_f)
+                   : share_cents(full, n, cents_f);
+    }
+  }
   if (want_rate) rate = cents / 100.0;  // exact float64 rate (base.py:435)
   const float rate_f = cents_f * 0.01f;  // the obs value
   double util = 0.0;
@@ -1261,7 +1267,7 @@ __device__ __forceinline__ void flush_staged(const KOut& out, const float* srew,
   __syncthreads();
 }
 
-template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM, int SCN = 0>
+template <bool PER_ENV_BS, bool LEAN, int UC, int LDSM, int SCN = 0, bool TF = false>
 __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -1379,7 +1385,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     const uint64_t envok_w = bal(env_ok), valid_w = bal(env_ok && m.u < U);
     for (int i = 0; i < nsteps; ++i) {
       const int sr = STG ? i % stage_rows : 0;
-      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG>(
+      moved |= packed_group<PER_ENV_BS, LEAN, UC, true, LDSM, SCN, STG, TF>(
           kp, st, out, tb, m, a, e, env_ok, hist, ltab, &pend, traj ? i : 0, lblob, lpcg,
           srew + sr * NWG + wvu * G, sdone + sr * NWG + wvu * G, envok_w, valid_w, lbs, nb_f);
       if (STG && (sr == stage_rows - 1 || i == nsteps - 1))
@@ -3566,8 +3572,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
     if (ldsm == 3 && lean) {  // a registered scenario's constants (scn_const)
       const int scn = match_scn(c);
-      if (scn == 1) kf = k_steps_packed<false, true, 15, 3, 1>;
-      if (scn == 2) kf = k_steps_packed<false, true, 30, 3, 2>;
+      const bool tf = c->tie_free != 0;  // (share_tie_free)
+      if (scn == 1) kf = tf ? k_steps_packed<false, true, 15, 3, 1, true> : k_steps_packed<false, true, 15, 3, 1>;
+      if (scn == 2) kf = tf ? k_steps_packed<false, true, 30, 3, 2, true> : k_steps_packed<false, true, 30, 3, 2>;
     }
     int nw = lds_waves(ldsm);
     if (ldsa)  // few groups: fewer waves per workgroup, the workgroups on every CU
