@@ -1963,12 +1963,13 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 }
 
 // LDS of k_steps_block (dynamic; sized by the host, block_lds_bytes): int2 keys[B + 2] (the
-// env's station keys), int cnt[2][B] (per-station connected-UE counts, two steps in flight),
-// int wt[4][16] (per-wave counts: need, active, connected, low QoE), double ps[4][16] (per-wave
-// partial sums: utility, rate, QoE, QoE^2), u128 slot[2] (stream state after the env's last
-// draw, increment), int tab[M] (the env's episode draw table), double r100[kMaxU + 1]
-// (100 / n correctly rounded: the ResourceFair share without a division, filled once per
-// workgroup).
+// env's station keys), int cnt[3][B] (per-station connected-UE counts, three steps in flight),
+// int wt[2][4][16] (per-wave counts by step parity: need, active, connected, low QoE), double
+// ps[2][4][16] (per-wave partial sums by step parity: utility, rate, QoE, QoE^2), u128 slot[2]
+// (stream state after the env's last draw, increment), int tab[M] (the env's episode draw
+// table), double r100[kMaxU + 1] (100 / n correctly rounded: the ResourceFair share without a
+// division, filled once per workgroup). The per-step buffers rotate so that ONE barrier per
+// step orders every producer before its consumers (k_steps_block).
 struct BlockLds {
   int2* key;
   int* cnt;
@@ -1983,7 +1984,7 @@ struct BlockLds {
 // then reads two stations per broadcast ds_read_b128 -- from the dynamic area it issued four
 // ds_read2_b32, twice the LDS cycles)
 __host__ __device__ inline size_t block_tab_off(int B) {
-  return ((8 * (size_t)B + 15) & ~(size_t)15) + 4 * 64 + 8 * 64 + 32;
+  return ((12 * (size_t)B + 15) & ~(size_t)15) + 4 * 128 + 8 * 128 + 32;
 }
 __host__ __device__ inline size_t block_r100_off(int B, int M) {
   return (block_tab_off(B) + 4 * (size_t)M + 15) & ~(size_t)15;
@@ -2020,11 +2021,11 @@ __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   l.key = keys;
   char* p = base;
   l.cnt = reinterpret_cast<int*>(p);
-  p += (8 * (size_t)B + 15) & ~(size_t)15;
+  p += (12 * (size_t)B + 15) & ~(size_t)15;
   l.wt = reinterpret_cast<int*>(p);
-  l.ps = reinterpret_cast<double*>(p + 4 * 64);
-  l.slot = reinterpret_cast<u128*>(p + 4 * 64 + 8 * 64);
-  l.tab = reinterpret_cast<int*>(p + 4 * 64 + 8 * 64 + 32);
+  l.ps = reinterpret_cast<double*>(p + 4 * 128);
+  l.slot = reinterpret_cast<u128*>(p + 4 * 128 + 8 * 128);
+  l.tab = reinterpret_cast<int*>(p + 4 * 128 + 8 * 128 + 32);
   return l;
 }
 
@@ -2053,18 +2054,18 @@ struct BlockRow {
 
 template <bool LEAN>
 __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& out,
-                                                 const BlockLds& L, int nw, int e, int row,
-                                                 const BlockRow& r) {
-  // the previous step's per-wave partials, summed in wave order (float64)
+                                                 const double* ps, const int* wt, int nw, int e,
+                                                 int row, const BlockRow& r) {
+  // the step's per-wave partials (its parity's buffers), summed in wave order (float64)
   double su = 0.0, sr = 0.0, sq = 0.0, sq2 = 0.0;
   int nlow = 0;
   for (int i = 0; i < nw; ++i) {
-    su += L.ps[i];
+    su += ps[i];
     if (!LEAN) {
-      sr += L.ps[16 + i];
-      sq += L.ps[32 + i];
-      sq2 += L.ps[48 + i];
-      nlow += L.wt[48 + i];
+      sr += ps[16 + i];
+      sq += ps[32 + i];
+      sq2 += ps[48 + i];
+      nlow += wt[48 + i];
     }
   }
   const double mean_u = r.nact > 0 ? su / (double)r.nact : kp.lower;
@@ -2091,9 +2092,9 @@ __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& 
 // doubles, exact), summed by the 64 lanes of wave 0 in one DPP tree (exact: integers below
 // 2^53, any order) instead of one lane's chain of dependent LDS reads; lane 63 writes.
 __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const KOut& out,
-                                                      const BlockLds& L, int nw, int e, int row,
+                                                      const double* ps, int nw, int e, int row,
                                                       const BlockRow& r, int lane) {
-  const double su = wave_sum_f64(lane < nw ? L.ps[lane] : 0.0);
+  const double su = wave_sum_f64(lane < nw ? ps[lane] : 0.0);
   if (lane == 63) {
     const double mean_u = r.nact > 0 ? (su * 0x1p-24) / (double)r.nact : kp.lower;
     const size_t re = (size_t)row * kp.E + e;
@@ -2105,16 +2106,24 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
 // nsteps steps of MComCore.step (base.py:230-296) for U > 64: one workgroup of ceil(U/64)
 // waves per env (lane u = UE u), envs e = blockIdx.x, blockIdx.x + gridDim.x, ...; each env's
 // state stays in registers / LDS for the launch (loaded once, stored once) and every step's
-// outputs go to row i of the trajectory (traj) or over the previous step's. Per step:
-//   A  lazy auto-reset (initial positions from the LDS draw table), need / active ballots
-//   -- barrier 1 --  workgroup scan of the waypoint draws (ue_id order); the previous step's
-//      per-env row (reward, done, metrics) by lane 0 from the per-wave partial sums
+// outputs go to row i of the trajectory (traj) or over the previous step's. Per step, ONE
+// workgroup barrier:
+//   A  lazy auto-reset (initial positions from the LDS draw table), need / active; the
+//      workgroup scan of the waypoint draws (ue_id order) from the per-wave counts the
+//      previous step wrote before its barrier
 //   B  waypoint draws (LDS draw table; beyond it, the stream state), move, association (the
-//      env's station keys in LDS, broadcast reads), per-station counts by LDS atomics
-//   -- barrier 2 --
-//   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums
-// The per-station counts alternate between two LDS arrays (the next step's array is zeroed
-// in its B phase), so two barriers per step suffice.
+//      env's station keys in LDS, broadcast reads), per-station counts by LDS atomics; the
+//      NEXT step's per-wave need / active counts (its reset applied ahead: both follow from
+//      t + 1 and the waypoint after this move)
+//   -- barrier --
+//   C  ResourceFair share, rounded rate, utility, per-UE stores, per-wave partial sums; the
+//      previous step's per-env row (reward, done, metrics) from its partial sums
+// Ordering without a second barrier: the per-wave counts and partial sums alternate between
+// two buffers by step parity and the per-station counts rotate over three arrays (the array
+// zeroed in step i's B phase was last read in step i-2's C phase, before step i-1's
+// barrier); the rare stream-state path (draws past the table, resets without one) takes an
+// extra barrier, block-uniform, before it writes the slot the other waves read at the step's
+// start.
 template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0, bool TF = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
@@ -2189,6 +2198,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     if (CULL && u == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
     bool s_ok = true;  // the slot holds the state after the env's last draw
     BlockRow prev{0, 0, 0};
+    // step 0's per-wave need / active counts (its lazy reset applied ahead)
+    auto ahead_counts = [&](int tn, int2 wpn, int* wt) {
+      const bool rs = tn >= KPS(t_end);
+      const int t0 = rs ? 0 : tn;
+      const bool act = valid && t0 >= KPS(arr_start) && t0 < KPS(arr_exit) &&
+                       (KPS(first_step_active) || t0 != 0);
+      const uint64_t mn = bal(act && (rs || wpn.x < 0)), ma = bal(act);
+      if (lane == 0) {
+        wt[w] = __popcll(mn);
+        wt[16 + w] = __popcll(ma);
+      }
+    };
+    ahead_counts(t, wp, L.wt);
     __syncthreads();
     // (uniform; launches of >= 32 steps: the records cost about as much as 18 steps' full scans)
     const bool cull = CULL && scaled && nb > 0 && nsteps >= 32;
@@ -2234,13 +2256,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       __syncthreads();
     }
 
-    for (int i = 0; i < nsteps; ++i) {
+    for (int i = 0, par = 0, c3 = 0; i < nsteps; ++i) {
       const int row = traj ? i : 0;
-      int* cnt = L.cnt + (i & 1) * KPS(B);  // (B = count array stride; two arrays below)
+      int* cnt = L.cnt + c3 * KPS(B);  // (B = count array stride; three arrays, rotating)
+      int* const wt = L.wt + 64 * par;       // this step's per-wave counts
+      double* const ps = L.ps + 64 * par;    // this step's per-wave partial sums
       // ---- A: lazy auto-reset, ballots ------------------------------------------------
       const bool reset = t >= KPS(t_end);  // uniform
       int koff = 0;
-      u128 base = L.slot[0];  // read before barrier 1 (the slot is written after it)
+      u128 base = L.slot[0];  // read at the step's start (a write waits for an extra barrier)
       const u128 inc = L.slot[1];
       if (reset) {
         t = 0;
@@ -2263,23 +2287,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                           (KPS(first_step_active) || t != 0);
       const bool need = active && wp.x < 0;
       const uint64_t mneed = bal(need);
-      const uint64_t mact = bal(active);
-      if (lane == 0) {
-        L.wt[w] = __popcll(mneed);
-        L.wt[16 + w] = __popcll(mact);
-      }
-      __syncthreads();  // ---- barrier 1
 
-      const int scan_need = row_scan_i32(lane < nw ? L.wt[lane & 15] : 0);
-      const int scan_act = row_scan_i32(lane < nw ? L.wt[16 + (lane & 15)] : 0);
+      const int scan_need = row_scan_i32(lane < nw ? wt[lane & 15] : 0);
+      const int scan_act = row_scan_i32(lane < nw ? wt[16 + (lane & 15)] : 0);
       const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
       const int tot = __builtin_amdgcn_readlane(scan_need, nw - 1);
       const int nact = __builtin_amdgcn_readlane(scan_act, nw - 1);
-      if (LEAN ? (w == 0 && i > 0) : (u == 0 && i > 0)) {
-        if (LEAN) block_finish_row_lean(kp, out, L, nw, e, traj ? i - 1 : 0, prev, lane);
-        else block_finish_row<LEAN>(kp, out, L, nw, e, traj ? i - 1 : 0, prev);
-      }
-      int* cnt_next = L.cnt + ((i + 1) & 1) * KPS(B);
+      const int c3n = c3 == 2 ? 0 : c3 + 1;
+      int* cnt_next = L.cnt + c3n * KPS(B);  // (last read in step i - 2)
       for (int k = u; k < KPS(B); k += blockDim.x) cnt_next[k] = 0;
 
       // ---- B: waypoint draws in ue_id order (movement.py:44-47), move ------------------
@@ -2294,7 +2309,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           s_ok = false;
         } else {
           // beyond the table (or none): from the stream state after pair bidx - 1 (the slot,
-          // or the table's last entry), pair k at offset 2 (k - bidx)
+          // or the table's last entry), pair k at offset 2 (k - bidx); every wave has read
+          // the slot before it is written (block-uniform branch)
+          __syncthreads();
           int bidx = drawn;
           if (M && !s_ok) {
             base = tb.tab_st[(size_t)e * M + (M - 1)];
@@ -2315,10 +2332,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           s_ok = true;
         }
         drawn += tot;
-      } else if (reset && !M && u == U - 1) {  // reset without draws: after the initial pairs
-        L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+      } else if (reset && !M) {  // reset without draws: after the initial pairs (uniform)
+        __syncthreads();
+        if (u == U - 1)
+          L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
       }
       if (active) move_ue_p(pos, wp, mp);
+      ahead_counts(t + 1, wp, L.wt + 64 * (par ^ 1));  // the next step's, after this move
 
       // ---- association: min over the env's station keys (LDS broadcast reads) ----------
       // (ext_vector_type loads: one broadcast ds_read_b128 per two stations; HIP's int4 struct is
@@ -2389,9 +2409,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       if (srv >= 0) atomicAdd(&cnt[srv], 1);
       if (!LEAN) {
         const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
-        if (lane == 0) L.wt[32 + w] = nc;
+        if (lane == 0) wt[32 + w] = nc;
       }
-      __syncthreads();  // ---- barrier 2
+      __syncthreads();  // ---- the step's barrier
       // the rate gather is waited for here (after the barrier: its latency overlaps the wait for
       // the other waves), on every path, before this step's stores: a lane or wave that never
       // reads `full` would carry the load as pending to a later merge, whose vmcnt(0) (before
@@ -2431,10 +2451,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       }
       if (LEAN) {  // 2^-24 fixed point: |sum| <= 64 * 2^24 (block_finish_row_lean)
         const int isu = wave_isum(active ? (int)((float)util * 0x1p24f) : 0);
-        if (lane == 63) L.ps[w] = (double)isu;
+        if (lane == 63) ps[w] = (double)isu;
       } else {
         const double su = wave_sum_f64(active ? util : 0.0);
-        if (lane == 63) L.ps[w] = su;
+        if (lane == 63) ps[w] = su;
       }
       if (!LEAN) {
         const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
@@ -2443,24 +2463,34 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const double sq2 = wave_sum_f64(active ? q * q : 0.0);
         const int nlow = __popcll(bal(active && q < kp.qoe_low));
         if (lane == 63) {
-          L.ps[16 + w] = sr;
-          L.ps[32 + w] = sq;
-          L.ps[48 + w] = sq2;
-          L.wt[48 + w] = nlow;
+          ps[16 + w] = sr;
+          ps[32 + w] = sq;
+          ps[48 + w] = sq2;
+          wt[48 + w] = nlow;
         }
       }
       int ncon = 0;
       if (!LEAN) {
-        const int sc = row_scan_i32(lane < nw ? L.wt[32 + (lane & 15)] : 0);
+        const int sc = row_scan_i32(lane < nw ? wt[32 + (lane & 15)] : 0);
         ncon = __builtin_amdgcn_readlane(sc, nw - 1);
+      }
+      // the previous step's per-env row (its partial sums are complete: written before this
+      // step's barrier)
+      if (LEAN ? (w == 0 && i > 0) : (u == 0 && i > 0)) {
+        const double* pps = L.ps + 64 * (par ^ 1);
+        if (LEAN) block_finish_row_lean(kp, out, pps, nw, e, traj ? i - 1 : 0, prev, lane);
+        else block_finish_row<LEAN>(kp, out, pps, L.wt + 64 * (par ^ 1), nw, e, traj ? i - 1 : 0, prev);
       }
       prev = BlockRow{t + 1, nact, ncon};
       t += 1;
+      par ^= 1;
+      c3 = c3n;
     }
     __syncthreads();  // the last step's partial sums
     if (LEAN ? (w == 0 && nsteps > 0) : (u == 0 && nsteps > 0)) {
-      if (LEAN) block_finish_row_lean(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev, lane);
-      else block_finish_row<LEAN>(kp, out, L, nw, e, traj ? nsteps - 1 : 0, prev);
+      const int lp = (nsteps - 1) & 1;  // the last step's parity
+      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nw, e, traj ? nsteps - 1 : 0, prev, lane);
+      else block_finish_row<LEAN>(kp, out, L.ps + 64 * lp, L.wt + 64 * lp, nw, e, traj ? nsteps - 1 : 0, prev);
     }
     // ---- epilogue: the state after the last step ----------------------------------------
     if (valid) store_ue(st.ue_state + idx, pos, wp);
