@@ -18,7 +18,8 @@ if [ -z "$SKIP_PROFILE" ]; then
 fi
 i=0
 for b in "$CUSTOM" "$PERENV" "--workload mobile-medium-central-v0 --envs 4096" \
-         "--workload mobile-large-ma-v0 --envs 32768" "--workload mobile-small-central-v0 --envs 65536"; do
+         "--workload mobile-large-ma-v0 --envs 32768" "--workload mobile-small-central-v0 --envs 65536" \
+         "--engine scenario_constants=-1"; do  # (the last: the headline on the generic instance)
   timeout -k 10 300 python bench.py $b --no-cpu-baseline > gpurun_out/bench_cfg_$i.log 2>&1 \
     || { echo "bench $b failed"; tail -30 gpurun_out/bench_cfg_$i.log; exit 1; }
   echo "== $b"; tail -1 gpurun_out/bench_cfg_$i.log
