@@ -74,7 +74,8 @@ struct KParams {
   float move_band;    // tie band of the float32 movement fast path
   float move_lim;     // 0.5 - move_band (exact)
   float u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale, u_offset;  // float32 utility
-  int axis_exact;     // (velocity * a) / a == velocity for every axis distance a
+  int axis_exact;     // 1: (velocity * a) / a == velocity for every axis distance a; 2: velocity
+                      // 1.5 on a map <= 1024 (the exact integer step, step_v15)
   float vel_f;
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
@@ -245,7 +246,7 @@ struct ScnConst {
   int cull_log, cull_nx, cull_nc;
 };
 __host__ __device__ constexpr ScnConst scn_const(int scn) {
-#define MEV_SCN_F32 2, 1, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
+#define MEV_SCN_F32 2, 2, 0x3fc00000u, 0x3efffd00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u, \
                     0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u, 19362
   // (LDS tables of mode 3 for 200 x 200: cell entries [0, 80000), 100/n at 80000, rates at
   // 80576, 113344 bytes in all)
@@ -277,6 +278,20 @@ __device__ __forceinline__ int2 move_exact(int2 pos, int dx, int dy, double vel)
 }
 
 
+// Velocity 1.5 (the registered scenarios' and mobile-env's default) in integers, exactly
+// (MoveP::axis_exact == 2, or the scenario instances' constants): off the axes
+// |q| = 1.5 |dx| / |v| lies strictly between 0 and 1.5, and |q| > 1/2 <=> 8 dx^2 > dy^2
+// (equality has no integer solution but 0, and |q| stays > 1e-7 away from 1/2 for coordinates
+// < 1024, far beyond float64's rounding of the reference's expression), so the step is
+// sgn(dx) [8 dx^2 > dy^2]; on an axis q = +-1.5 exactly, and np.round's half-to-even gives
+// |step| 2 from an even coordinate, 1 from an odd one. (Arrival, d2 <= 2, is the caller's;
+// tests/test_oracle.py checks the formula against the reference expression for every
+// displacement of a 200 x 200 map.)
+__device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int ay2) {
+  const int sx = (ax2 << 3 > ay2 ? 1 : 0) + (dy == 0 && !(pos.x & 1) ? 1 : 0);
+  const int sy = (ay2 << 3 > ax2 ? 1 : 0) + (dx == 0 && !(pos.y & 1) ? 1 : 0);
+  return make_int2(pos.x + (dx < 0 ? -sx : sx), pos.y + (dy < 0 ? -sy : sy));
+}
 // Movement step. Arrival (|v| <= velocity) is the integer test d2 <= d2snap (sqrt is
 // correctly rounded and monotone). Otherwise the new coordinate is x + rint(q) with
 // q = velocity * dx / |v| (x is an integer, so rint(x + q) = x + rint(q) unless x + q is a
@@ -293,6 +308,10 @@ __device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) 
   if (d2 <= mp.d2snap) {  // arrived: snap to waypoint and pop it
     pos = wp;
     wp = make_int2(-1, -1);
+    return;
+  }
+  if (mp.axis_exact == 2) {  // velocity 1.5: integers (step_v15)
+    pos = step_v15(pos, dx, dy, __mul24(dx, dx), __mul24(dy, dy));
     return;
   }
   if (mp.axis_exact && (dx == 0 || dy == 0)) {
@@ -316,19 +335,6 @@ __device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) 
 }
 
 // The context's movement parameters (compile-time constants in a scenario instance).
-// Velocity 1.5 (the registered scenarios' constants) in integers, exactly: off the axes
-// |q| = 1.5 |dx| / |v| lies strictly between 0 and 1.5, and |q| > 1/2 <=> 8 dx^2 > dy^2
-// (equality has no integer solution but 0, and |q| stays > 1e-7 away from 1/2 for coordinates
-// < 1024, far beyond float64's rounding of the reference's expression), so the step is
-// sgn(dx) [8 dx^2 > dy^2]; on an axis q = +-1.5 exactly, and np.round's half-to-even gives
-// |step| 2 from an even coordinate, 1 from an odd one. (Arrival, d2 <= 2, is the caller's;
-// tests/test_oracle.py checks the formula against the reference expression for every
-// displacement of a 200 x 200 map.)
-__device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int ay2) {
-  const int sx = (ax2 << 3 > ay2 ? 1 : 0) + (dy == 0 && !(pos.x & 1) ? 1 : 0);
-  const int sy = (ay2 << 3 > ax2 ? 1 : 0) + (dx == 0 && !(pos.y & 1) ? 1 : 0);
-  return make_int2(pos.x + (dx < 0 ? -sx : sx), pos.y + (dy < 0 ? -sy : sy));
-}
 template <int SCN>
 constexpr bool scn_v15() { return SCN != 0 && scn_const(SCN).vel_f == 0x3fc00000u; }
 // Every UE active at every step (a scenario with arrival at 0, no departure before the episode
@@ -1564,7 +1570,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     const int ax2 = __mul24(dx, dx), ay2 = __mul24(dy, dy);
     const int d2 = ax2 + ay2;
     arrive[r] = d2 <= KPS(d2snap);
-    if constexpr (V15) {
+    if (V15 || KPS(axis_exact) == 2) {  // (generic instances: a uniform branch)
       npos[r] = arrive[r] ? wp : step_v15(pos, dx, dy, ax2, ay2);
       continue;
     }
@@ -3117,6 +3123,8 @@ static MoveP host_move_params(double velocity, int W, int H) {
   const int amax = W > H ? W : H;
   for (int a = 1; a <= amax; ++a)
     if ((velocity * (double)a) / (double)a != velocity) mp.axis_exact = 0;
+  // velocity 1.5 on maps up to 1024: the exact integer step (step_v15)
+  if (velocity == 1.5 && W <= 1024 && H <= 1024) mp.axis_exact = 2;
   return mp;
 }
 
