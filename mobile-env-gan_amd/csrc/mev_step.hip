@@ -1480,7 +1480,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   }
   bool valid[R], active[R], need[R], do_reset[R], reset_env[R];
   int tot[R], rank[R];
-  uint64_t act_w[R], mneed_w[R];
+  uint64_t act_w[R], mneed_w[R], rs_w[R];
   // ---- A: lazy auto-reset, ballots (base.py:288-291) ----------------------------------------
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -1488,7 +1488,8 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     valid[r] = kval < nok[r];
     reset_env[r] = env_ok[r] && c[r].t >= KPS(t_end);
     do_reset[r] = reset_env[r] && valid[r];
-    if (bal(c[r].t >= KPS(t_end)) & envok_w[r]) {  // initial positions = the episode's first U
+    rs_w[r] = bal(c[r].t >= KPS(t_end)) & envok_w[r];
+    if (rs_w[r]) {  // initial positions = the episode's first U
       if (reset_env[r]) {                          // pairs of the draw table
         c[r].t = 0;
         c[r].drawn = U;
@@ -1548,13 +1549,17 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
         wait_vmem();
       }
     }
-    const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
-                         (do_reset[r] && tot[r] == 0 && u == U - 1);
-    if (fell_back && own_fin) slot[0] = s_fin;
-    if (fell_back && tot[r] > 0) c[r].s_ok = true;
-    else if (tot[r] > 0 || reset_env[r]) c[r].s_ok = false;
-    c[r].moved |= own_fin;
-    c[r].drawn += tot[r];
+    // the stream bookkeeping, only where a draw or a reset happened (uniform; without either
+    // nothing changes, and the per-lane masks cost ~15 SALU per group)
+    if (mneed_w[r] | rs_w[r]) {
+      const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
+                           (do_reset[r] && tot[r] == 0 && u == U - 1);
+      if (fell_back && own_fin) slot[0] = s_fin;
+      if (fell_back && tot[r] > 0) c[r].s_ok = true;
+      else if (tot[r] > 0 || reset_env[r]) c[r].s_ok = false;
+      c[r].moved |= own_fin;
+      c[r].drawn += tot[r];
+    }
   }
   // ---- C: movement (movement.py:49-62), branch-free fast path --------------------------------
   // (move_ue_p per lane: arrival snap; axis-parallel moves exactly in float32 when the velocity
@@ -1571,7 +1576,11 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     const int d2 = ax2 + ay2;
     arrive[r] = d2 <= KPS(d2snap);
     if (V15 || KPS(axis_exact) == 2) {  // (generic instances: a uniform branch)
-      npos[r] = arrive[r] ? wp : step_v15(pos, dx, dy, ax2, ay2);
+      // the step for every lane, then a select: as a branch on `arrive` (nearly every lane
+      // moves) the compiler spent three SALU on exec masks per group and step
+      int2 np = step_v15(pos, dx, dy, ax2, ay2);
+      asm volatile("" : "+v"(np.x), "+v"(np.y));
+      npos[r] = arrive[r] ? wp : np;
       continue;
     }
     const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);
@@ -1594,11 +1603,10 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     npos[r] = arrive[r] ? wp : np;
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (active[r]) {  // (selects)
-      c[r].pos = npos[r];
-      if (arrive[r]) c[r].wp = make_int2(-1, -1);
-    }
+  for (int r = 0; r < R; ++r) {  // selects (an `if` here became an exec-mask branch)
+    const bool pop = active[r] && arrive[r];
+    c[r].pos = active[r] ? npos[r] : c[r].pos;
+    c[r].wp = pop ? make_int2(-1, -1) : c[r].wp;
   }
   // ---- D: association, n_b, share, utility ---------------------------------------------------
   int srv[R];
