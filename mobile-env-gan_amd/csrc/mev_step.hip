@@ -74,8 +74,10 @@ struct KParams {
   float move_band;    // tie band of the float32 movement fast path
   float move_lim;     // 0.5 - move_band (exact)
   float u_log2_coef, u_w2f, u_lowerf, u_upperf, u_scale, u_offset;  // float32 utility
-  int axis_exact;     // 1: (velocity * a) / a == velocity for every axis distance a; 2: velocity
-                      // 1.5 on a map <= 1024 (the exact integer step, step_v15)
+  int axis_exact;     // 1: (velocity * a) / a == velocity for every axis distance a and the
+                      // velocity not an integer (axis moves = pos +- velocity, ties for the
+                      // fast path: a float64 add instead); 2: velocity 1.5 on a map <= 1024
+                      // (the exact integer step, step_v15); 0: neither (integer velocities)
   float vel_f;
   int xcd_remap;      // 1: blocks sharing an XCD (blockIdx % 8) take one contiguous env range
   // LDS association tables of a shared layout (fused launches; 0: off, see KTables::lds_blob)
@@ -260,7 +262,7 @@ __host__ __device__ constexpr ScnConst scn_const(int scn) {
                              MEV_SCN_F32}
        // mobile-custom-128x1024-v0 (block kernel): velocity 10 (d2snap 100, float32 10, tie
        // band 2^-16 x 10), draw table 3U + 8, no LDS tables, default channel and utility
-       : scn == 4 ? ScnConst{1024, 128, 200, 200, 3080, 0, 20, 0, 20, 1, 0, 0, 0, 0, 100, 1,
+       : scn == 4 ? ScnConst{1024, 128, 200, 200, 3080, 0, 20, 0, 20, 1, 0, 0, 0, 0, 100, 0,
                              0x41200000u, 0x3effec00u, 0x3ba3d70au, 0x3ba3d70au, 0x4040a8c1u,
                              0x00000000u, 0xc1a00000u, 0x41a00000u, 0x3d4ccccdu, 0x00000000u,
                              19362, 2, 50, 2500}
@@ -299,7 +301,8 @@ __device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int 
 // absolute error is < 5e-7 * max(1, velocity)); only when q lies within move_band =
 // 2^-16 * max(1, velocity) (30x wider) of a half-integer -- where float32 could pick the
 // other integer, or half-to-even needs the exact value -- is the exact float64 form used. Axis-parallel
-// moves (q = +-velocity exactly) are done exactly in float64 (no division needed).
+// moves at a non-integer velocity (q = +-velocity exactly, often a tie) are done exactly in
+// float64 (no division needed); at an integer velocity the fast path gives them.
 __device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) {
   const int dx = wp.x - pos.x;
   const int dy = wp.y - pos.y;
@@ -3131,6 +3134,9 @@ static MoveP host_move_params(double velocity, int W, int H) {
   const int amax = W > H ? W : H;
   for (int a = 1; a <= amax; ++a)
     if ((velocity * (double)a) / (double)a != velocity) mp.axis_exact = 0;
+  // an integer velocity: an axis move is pos +- velocity, no tie, and the float32 fast path
+  // (q = +-velocity within 5e-7 relative, far from a half-integer) gives it -- no axis branch
+  if (velocity == floor(velocity) && velocity <= 0x1p20) mp.axis_exact = 0;
   // velocity 1.5 on maps up to 1024: the exact integer step (step_v15)
   if (velocity == 1.5 && W <= 1024 && H <= 1024) mp.axis_exact = 2;
   return mp;
@@ -3240,13 +3246,11 @@ static KTables tables_of(const mev_ctx* c) {
   return tb;
 }
 
-int mev_create(const mev_params* params, mev_ctx** out) {
-  if (!out) return MEV_EINVAL;
-  *out = nullptr;
-  int rc = validate(params);
-  if (rc) return rc;
-  mev_ctx* c = new (std::nothrow) mev_ctx();
-  if (!c) return MEV_ENOMEM;
+// The body of mev_create on a value-initialised context; on any failure the caller releases
+// what was allocated so far (mev_destroy takes a partly built context), so every early return
+// -- a HIP error included -- leaves nothing behind.
+static int create_ctx(mev_ctx* c, const mev_params* params) {
+  int rc = 0;
   c->p = *params;
   MEV_HIP(hipGetDevice(&c->device));
 
@@ -3319,7 +3323,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     c->kp.d2max = -1;
     rc = build_het(c);
     if (rc) {
-      mev_destroy(c);
       return rc;
     }
   } else {
@@ -3329,7 +3332,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     if (tab == nullptr) {
       n = mev_build_rate_table(params, nullptr, 0);
       if (n < 0) {
-        mev_destroy(c);
         return (int)n;
       }
       host.resize((size_t)std::max<int64_t>(n, 1));
@@ -3340,7 +3342,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     c->kp.d2max = c->d2max;
     // (one entry at least: lanes without a server read entry 0 unconditionally)
     if (hipMalloc(&c->rate_full, sizeof(double) * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) {
-      mev_destroy(c);
       return MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(c->rate_full, 0, sizeof(double)));
@@ -3360,7 +3361,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
         hipMalloc(&c->tab_st, sizeof(u128) * n) != hipSuccess ||
         hipMalloc(&c->drawn, sizeof(int) * (size_t)params->num_envs) != hipSuccess) {
       const bool bad = c->kp.tab_m < params->num_ues || n >= ((size_t)1 << 28);
-      mev_destroy(c);
       return bad ? MEV_EINVAL : MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(c->drawn, 0, sizeof(int) * (size_t)params->num_envs));
@@ -3369,7 +3369,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   // ---- PCG64 jump table: offsets up to 2U (reset) + 2U (waypoints), and the table pairs --
   c->jmax = max(4 * params->num_ues, 2 * c->kp.tab_m + 2);
   if (hipMalloc(&c->jump, sizeof(u128) * 2 * (size_t)(c->jmax + 1)) != hipSuccess) {
-    mev_destroy(c);
     return MEV_ENOMEM;
   }
   hipLaunchKernelGGL(k_jump_table, dim3((c->jmax + 256) / 256), dim3(256), 0, 0, c->jmax,
@@ -3382,7 +3381,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   if (!params->bs_per_env && !c->kp.het) {
     const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height;
     if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
-      mev_destroy(c);
       return MEV_ENOMEM;
     }
     MEV_HIP(hipMemset(c->assoc, 0xff, bytes));  // srv -1 everywhere until a layout is set
@@ -3390,7 +3388,6 @@ int mev_create(const mev_params* params, mev_ctx** out) {
   if (!c->kp.het) {  // LDS tables: shared layouts (modes 1-3), per-env layouts (mode 4)
     rc = build_lds_tables(c);
     if (rc) {
-      mev_destroy(c);
       return rc;
     }
   }
@@ -3403,18 +3400,20 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     if (hipMalloc(&c->util, sizeof(double) * (size_t)(kmax + 1)) != hipSuccess ||
         hipMalloc(&d_bad, sizeof(int)) != hipSuccess) {
       if (d_bad) (void)hipFree(d_bad);
-      mev_destroy(c);
       return MEV_ENOMEM;
     }
+    struct DevFree {  // d_bad is released on every path out of this block
+      int* q;
+      ~DevFree() { (void)hipFree(q); }
+    } bad_guard{d_bad};
     MEV_HIP(hipMemset(d_bad, 0, sizeof(int)));
     hipLaunchKernelGGL(k_util_table, dim3((kmax + 256) / 256), dim3(256), 0, 0, c->kp, kmax,
                        c->util, d_bad);
     MEV_HIP(hipGetLastError());
     int bad = 0;
     MEV_HIP(hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost));
-    MEV_HIP(hipFree(d_bad));
     if (bad) {  // not saturated at kmax: fall back to in-kernel evaluation
-      MEV_HIP(hipFree(c->util));
+      (void)hipFree(c->util);
       c->util = nullptr;
       c->kp.util_direct = 1;
     }
@@ -3431,7 +3430,21 @@ int mev_create(const mev_params* params, mev_ctx** out) {
     MEV_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   }
   MEV_HIP(hipDeviceSynchronize());
+  return MEV_OK;
+}
 
+int mev_create(const mev_params* params, mev_ctx** out) {
+  if (!out) return MEV_EINVAL;
+  *out = nullptr;
+  const int rc0 = validate(params);
+  if (rc0) return rc0;
+  mev_ctx* c = new (std::nothrow) mev_ctx();
+  if (!c) return MEV_ENOMEM;
+  const int rc = create_ctx(c, params);
+  if (rc) {
+    mev_destroy(c);
+    return rc;
+  }
   *out = c;
   return MEV_OK;
 }

@@ -286,3 +286,43 @@ def test_store_hazard_check_on_generated_assembly():
     text = open(ch.build_asm()).read()
     assert ch.wide_store_count(text) > 0
     assert ch.violations(text) == []
+
+
+def test_host_code_under_asan(tmp_path, golden_dir):
+    """The library's host code (argument checks, numpy-compatible seeding, the libm channel
+    table, mev_create's validation and failure path) under AddressSanitizer + UBSan with leak
+    detection: `make asan` builds libmev_asan.so (sanitizers on the host side only), and
+    tests/asan/host_driver.c calls every entry point that needs no GPU with exactly sized
+    buffers. Its printed seed rows must equal numpy's PCG64 seeding and its table the
+    reference's channel table (channel_default.npz)."""
+    import shutil
+    import subprocess
+    clang = "/opt/rocm/llvm/bin/clang"
+    if not os.path.exists(clang) or shutil.which("make") is None:
+        pytest.skip("ROCm clang / make not available")
+    csrc = os.path.join(ROOT, "mobile-env-gan_amd", "csrc")
+    subprocess.run(["make", "-s", "-C", csrc, "asan"], check=True, timeout=900)
+    lib = os.path.join(ROOT, "mobile-env-gan_amd", "lib", "libmev_asan.so")
+    drv = str(tmp_path / "host_driver")
+    subprocess.run([clang, "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-g",
+                    "-I", os.path.join(ROOT, "include"), "-o", drv,
+                    os.path.join(ROOT, "tests", "asan", "host_driver.c"), lib,
+                    "-Wl,-rpath," + os.path.dirname(lib)], check=True, timeout=120)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([drv], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
+    lines = r.stdout.split("\n")
+    assert "ok" in lines
+    for ln in (x for x in lines if x.startswith("seed ")):
+        seed, slo, shi, ilo, ihi = (int(v) for v in ln.split()[1:])
+        st = np.random.PCG64(seed).state["state"]
+        assert (shi << 64 | slo) == st["state"] and (ihi << 64 | ilo) == st["inc"], seed
+    n, t1, tmid, tlast = next(x for x in lines if x.startswith("table ")).split()[1:]
+    c = np.load(f"{golden_dir}/channel_default.npz")
+    rate = c["rate"]
+    assert int(n) == int(c["d2max"]) + 1 == len(rate)
+    # (the C library's log10 may differ from numpy's by an ulp: the Python host passes numpy's)
+    np.testing.assert_allclose([float(t1), float(tmid), float(tlast)],
+                               [rate[1], rate[int(n) // 2], rate[-1]], rtol=1e-14)
