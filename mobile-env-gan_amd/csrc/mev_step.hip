@@ -1708,7 +1708,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   for (int r = 0; r < R; ++r) {
     const float rate_f = cf[r] * 0.01f;
     const float util = active[r] ? (float)utility_f32r<SCN>(cf[r], rate_f, kp) : 0.f;
-    const int isum = seg_isum_rows<PC>(active[r] ? (int)(util * 0x1p25f) : 0);
+    const int isum = seg_isum_rows<PC>((int)(util * 0x1p25f));  // (util = 0 where inactive)
     const int nact = __popc(seg_field<PC>(act_w[r], m));
     Pending up;
     up.srv = srv[r];
@@ -1981,7 +1981,7 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 
 // LDS of k_steps_block (dynamic; sized by the host, block_lds_bytes): int2 keys[B + 2] (the
 // env's station keys), int cnt[3][B] (per-station connected-UE counts, three steps in flight),
-// int wt[2][4][16] (per-wave counts by step parity: need, active, connected, low QoE), double
+// int wt[2][4][16] (per-wave counts by step parity: need | active << 16, -, connected, low QoE), double
 // ps[2][4][16] (per-wave partial sums by step parity: utility, rate, QoE, QoE^2), u128 slot[2]
 // (stream state after the env's last draw, increment), int tab[M] (the env's episode draw
 // table), double r100[kMaxU + 1] (100 / n correctly rounded: the ResourceFair share without a
@@ -2222,10 +2222,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const bool act = valid && t0 >= KPS(arr_start) && t0 < KPS(arr_exit) &&
                        (KPS(first_step_active) || t0 != 0);
       const uint64_t mn = bal(act && (rs || wpn.x < 0)), ma = bal(act);
-      if (lane == 0) {
-        wt[w] = __popcll(mn);
-        wt[16 + w] = __popcll(ma);
-      }
+      // {need, active} packed in one int (each <= 64 per wave, <= 1024 per env): one read
+      // and one scan per step
+      if (lane == 0) wt[w] = __popcll(mn) | (__popcll(ma) << 16);
     };
     ahead_counts(t, wp, L.wt);
     __syncthreads();
@@ -2281,8 +2280,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // ---- A: lazy auto-reset, ballots ------------------------------------------------
       const bool reset = t >= KPS(t_end);  // uniform
       int koff = 0;
-      u128 base = L.slot[0];  // read at the step's start (a write waits for an extra barrier)
-      const u128 inc = L.slot[1];
+      // the stream slot {state, increment}: read only on the rare paths that draw from it, and
+      // there before the branch's barrier (the slot's write follows that barrier)
+      u128 base = 0, inc = 0;
       if (reset) {
         t = 0;
         wp = make_int2(-1, -1);
@@ -2294,6 +2294,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           drawn = U;
           s_ok = false;
         } else {
+          base = L.slot[0];
+          inc = L.slot[1];
           const ulonglong2 c = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
           if (kp.movement_reseed) base = mk128(c.x, c.y);
           if (valid) (void)pcg_draw_pair(base, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
@@ -2305,14 +2307,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const bool need = active && wp.x < 0;
       const uint64_t mneed = bal(need);
 
-      const int scan_need = row_scan_i32(lane < nw ? wt[lane & 15] : 0);
-      const int scan_act = row_scan_i32(lane < nw ? wt[16 + (lane & 15)] : 0);
-      const int pre_need = w ? __builtin_amdgcn_readlane(scan_need, w - 1) : 0;
-      const int tot = __builtin_amdgcn_readlane(scan_need, nw - 1);
-      const int nact = __builtin_amdgcn_readlane(scan_act, nw - 1);
+      const int scan_na = row_scan_i32(lane < nw ? wt[lane & 15] : 0);
+      const int pre_need = w ? (__builtin_amdgcn_readlane(scan_na, w - 1) & 0xffff) : 0;
+      const int tot_na = __builtin_amdgcn_readlane(scan_na, nw - 1);
+      const int tot = tot_na & 0xffff;
+      const int nact = tot_na >> 16;
       const int c3n = c3 == 2 ? 0 : c3 + 1;
       int* cnt_next = L.cnt + c3n * KPS(B);  // (last read in step i - 2)
-      for (int k = u; k < KPS(B); k += blockDim.x) cnt_next[k] = 0;
+      if (SCN) {  // (a scenario instance: U >= B, one store per lane)
+        static_assert(!SCN || scn_const(SCN).U >= scn_const(SCN).B, "block scenario: U >= B");
+        if (u < KPS(B)) cnt_next[u] = 0;
+      } else {
+        for (int k = u; k < KPS(B); k += blockDim.x) cnt_next[k] = 0;
+      }
 
       // ---- B: waypoint draws in ue_id order (movement.py:44-47), move ------------------
       const int rank = pre_need + (int)__popcll(mneed & lt);
@@ -2328,6 +2335,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           // beyond the table (or none): from the stream state after pair bidx - 1 (the slot,
           // or the table's last entry), pair k at offset 2 (k - bidx); every wave has read
           // the slot before it is written (block-uniform branch)
+          if (!(reset && !M)) {  // (a reset without a table read it above)
+            base = L.slot[0];
+            inc = L.slot[1];
+          }
           __syncthreads();
           int bidx = drawn;
           if (M && !s_ok) {
@@ -2467,7 +2478,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         }
       }
       if (LEAN) {  // 2^-24 fixed point: |sum| <= 64 * 2^24 (block_finish_row_lean)
-        const int isu = wave_isum(active ? (int)((float)util * 0x1p24f) : 0);
+        const int isu = wave_isum((int)((float)util * 0x1p24f));  // (util = 0 where inactive)
         if (lane == 63) ps[w] = (double)isu;
       } else {
         const double su = wave_sum_f64(active ? util : 0.0);
