@@ -2300,6 +2300,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           if (kp.movement_reseed) base = mk128(c.x, c.y);
           if (valid) (void)pcg_draw_pair(base, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
           koff = 2 * U;
+          wait_vmem();
         }
       }
       const bool active = valid && t >= KPS(arr_start) && t < KPS(arr_exit) &&
@@ -2344,6 +2345,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           if (M && !s_ok) {
             base = tb.tab_st[(size_t)e * M + (M - 1)];
             bidx = M;
+            // (waited for here: a load left pending into the common path's merge makes the
+            // compiler's vmcnt(0) there wait for the previous step's stores as well)
+            wait_vmem();
           }
           if (need) {
             u128 s_fin;
