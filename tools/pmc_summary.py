@@ -7,9 +7,9 @@ comes back with the call, and tools/merge_profiles.py folds it into profiles/)
 
 Reads the rocprofv3 CSVs of the passes (kt: kernel trace + stats; fetch / write / sq / sq2: PMC
 counters) and keeps the dispatches of the launch the bench times:
-  * --launch fused (default): the fused multi-step kernel k_steps_packed (--chunk steps each,
-    one dispatch per chunk);
-  * --launch single / split: the one-step kernels k_step_packed / k_step_block.
+  * --launch fused (default): the fused multi-step kernel the launch selects -- k_steps_lds2,
+    k_steps_packed or k_steps_block (--chunk steps each, one dispatch per chunk);
+  * --launch single / split: the one-step kernels k_step_packed / k_steps_block (one step).
 Writes
   profiles/<tag>_kernel_stats.csv   -- rocprofv3 --stats summary (copied)
   profiles/<tag>_pmc.json           -- per-launch averages of every counter, timed-region
