@@ -2383,7 +2383,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // candidate (a per-lane ds_read_b64), until no lane of the wave has more
       bool full_scan = true;
       if (cull) {
-        const int cell = min((max(pos.y, 0) >> CLOG) * CNX + (max(pos.x, 0) >> CLOG), CNC - 1);
+        const int cell = min(__mul24(max(pos.y, 0) >> CLOG, CNX) + (max(pos.x, 0) >> CLOG), CNC - 1);
         const v4u32 rec = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
         const int cn = active ? (int)(rec.x & 255u) : 0;
         full_scan = bal(cn > 15) != 0;
@@ -2391,7 +2391,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
           // the first four candidates unconditionally (four reads in flight; past a lane's
           // count the record holds the padding index, whose key never wins), then one at a
-          // time while a lane of the wave has more
+          // time while a lane of the wave has more (two at a time: timing-neutral)
           auto key_of = [&](int j) {
             const unsigned wd = j < 3 ? rec.x : j < 7 ? rec.y : j < 11 ? rec.z : rec.w;
             const int2 kv = lds_keys[__builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u)];

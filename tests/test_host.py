@@ -326,3 +326,26 @@ def test_host_code_under_asan(tmp_path, golden_dir):
     # (the C library's log10 may differ from numpy's by an ulp: the Python host passes numpy's)
     np.testing.assert_allclose([float(t1), float(tmid), float(tlast)],
                                [rate[1], rate[int(n) // 2], rate[-1]], rtol=1e-14)
+
+
+@pytest.mark.parametrize("v", [1.0, 3.0, 10.0, 25.0, 100.0])
+def test_integer_velocity_axis_moves_take_the_fast_path(v):
+    """An integer velocity has no axis-parallel branch (host_move_params sets axis_exact 0,
+    mev_step.hip move_ue_p): an axis move is pos +- v in the reference (movement.py:58-62, the
+    float64 p + v * a / |a| is exact and integral), and the float32 fast path -- q = a * (v_f *
+    rsq(a^2)) with rsq within 2^-21 relative, accepted when |q - rint(q)| < 0.5 - 2^-16 max(1, v)
+    -- must accept every such move and give exactly +-v. Checked for every axis distance on a
+    1024 map beyond the arrival radius, at both ends of the rsq error bound."""
+    a = np.arange(1, 1024, dtype=np.float64)
+    a = a[a > v]  # |a| <= v: arrival (the snap), not a step
+    ref = np.rint(0.0 + (v * a) / np.sqrt(a * a))  # the reference's float64 step from p = 0
+    assert np.all(ref == v)
+    lim = np.float32(0.5 - 2.0 ** -16 * max(1.0, v))
+    for rel in (-(2.0 ** -21), 0.0, 2.0 ** -21):
+        rsq = ((1.0 / a) * (1.0 + rel)).astype(np.float32)
+        sc = np.float32(v) * rsq
+        for sgn in (1.0, -1.0):
+            q = (sgn * a).astype(np.float32) * sc
+            r = np.rint(q)
+            assert np.all(np.abs(q - r) < lim)
+            assert np.all(r == sgn * v)
