@@ -1445,6 +1445,10 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 // cells, episode resets) are wave-uniform branches per context. Same results as packed_group
 // bit for bit (tests). Shapes: U = 15 / 30 at compile time (aligned segments), lean outputs,
 // a draw table (tab_m > 0), staged per-env rows.
+// Per-env histogram stride of k_steps_lds2 (see lds2_per_wave): max(B + 1, P = 64 / G)
+__host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
+  return B + 1 > 64 / G ? B + 1 : 64 / G;
+}
 struct Ctx2 {
   int t, drawn;
   bool s_ok, moved;
@@ -1461,7 +1465,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                                           int* __restrict__ srow, uint8_t* __restrict__ drow,
                                           const int* __restrict__ lkeys) {
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
-  const int M = KPS(tab_m), B = KPS(B), HB = B + 1;
+  const int M = KPS(tab_m), B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
   // lanes UE u of segment s hold valid = u < U; wave masks of the envs that exist (nok[r] of
   // the group's G) from the uniform count, in SALU each step (kept loop-variant: hoisted, the
@@ -1673,9 +1677,9 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   int bin[R], n[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    h[r] = hist + (r * G + m.seg) * HB;
+    h[r] = hist + (r * G + m.seg) * HS;
     bin[r] = srv[r] >= 0 ? srv[r] : B;
-    h[r][min(u, B)] = 0;
+    h[r][HS >= PC ? u : min(u, B)] = 0;  // (u < PC: one word per lane)
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1722,11 +1726,12 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
     // the env's staged row entry: the 2^-25 fixed-point utility sum and {nact, done}; the
     // workgroup's flush forms the float32 reward from them. Lanes other than the env's last
-    // write into the histogram's spare bin instead (no branch).
+    // write into their own histogram word instead (no branch; re-zeroed next step).
     const bool lead = klead < nok[r];
     const int er = r * G + m.seg;
-    int* sw = lead ? srow + er : h[r] + B;
-    uint8_t* dw = lead ? drow + er : reinterpret_cast<uint8_t*>(h[r] + B);
+    int* const hw = h[r] + (HS >= PC ? u : B);
+    int* sw = lead ? srow + er : hw;
+    uint8_t* dw = lead ? drow + er : reinterpret_cast<uint8_t*>(hw);
     *sw = isum;
     *dw = (uint8_t)(nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0));
     c[r].t += 1;
@@ -1755,9 +1760,12 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
 }
 
 // LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, (PE) station keys [R G][16][2] int,
-// histograms [R G][B + 1] int, draw tables [R G][M] int
+// histograms [R G][HS] int, draw tables [R G][M] int. HS = max(B + 1, P): with a bin per lane
+// of the segment, the per-step zeroing and the non-leader lanes' dummy row writes go to
+// distinct words (at HS = B + 1 the lanes past B all hit bin B: same-word LDS writes)
 __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool PE = false) {
-  return sizeof(int) * (size_t)(R * G) * (8 + (PE ? 32 : 0) + (size_t)(B + 1) + (size_t)M);
+  return sizeof(int) * (size_t)(R * G) *
+         (8 + (PE ? 32 : 0) + (size_t)lds2_hist_stride(G, B) + (size_t)M);
 }
 
 // PE: per-env station layouts (KParams::lds_mode 4: the blob holds the rank index of S, 100/n
@@ -1789,9 +1797,10 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   constexpr int KB = PE ? 32 : 0;  // ints per env of staged station keys
   u128* lpcg = reinterpret_cast<u128*>(lw) + wv * R * G * 2;
   int* lkeys = lw + NW * R * G * 8 + wv * R * G * KB;
-  int* hist = lw + NW * R * G * (8 + KB) + wv * R * G * (B + 1);
-  int* ltab = lw + NW * R * G * (8 + KB + B + 1) + wv * R * G * M;
-  int* srow = lw + NW * R * G * (8 + KB + B + 1 + M);
+  const int HS = lds2_hist_stride(G, B);
+  int* hist = lw + NW * R * G * (8 + KB) + wv * R * G * HS;
+  int* ltab = lw + NW * R * G * (8 + KB + HS) + wv * R * G * M;
+  int* srow = lw + NW * R * G * (8 + KB + HS + M);
   uint8_t* drow = reinterpret_cast<uint8_t*>(srow + stage_rows * NWG);
   const int npairs = (ngroups + 1) / 2;
   const int gstride = (int)gridDim.x * NW;
