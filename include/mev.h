@@ -27,7 +27,13 @@
  *                                 {state_lo, state_hi, inc_lo, inc_hi,
  *                                  state0_lo, state0_hi}; state0 = state right after
  *                                 seeding (movement re-seeds each episode,
- *                                 movement.py:16-18 with reset_rng_episode=True)
+ *                                 movement.py:16-18 with reset_rng_episode=True).
+ *                                 With the episode draw table (draw_table) the
+ *                                 step kernels leave {state} as it is while the
+ *                                 episode's draws stay inside the table -- the
+ *                                 table holds the state then -- and write it
+ *                                 only after draws past it; mev_sync_stream_state
+ *                                 materialises it (checkpoints, comparisons)
  *       t       int32 [E]         episode time (base.py:175,280)
  *       bs_xy   int32 [B][2] (shared; the step kernel uses the keys derived from it by
  *                                 mev_reset / mev_update_stations) or [E][B][2] (per env);
@@ -52,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 13
+#define MEV_ABI_VERSION 14
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -232,6 +238,11 @@ int mev_reset(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
  * pcg rows' state0 (mev_reset does it; call it after changing pcg rows without a reset). */
 int mev_prepare_draws(const mev_ctx* ctx, const mev_state* state, const uint8_t* env_mask,
                       void* stream);
+
+/* Write every env's movement stream state (numpy PCG64 state after the env's draws so far,
+ * movement.py:44-47,64-72) into its pcg row: the step kernels skip that write while an
+ * episode's draws stay inside the episode draw table (mev_state.pcg). Stream-ordered. */
+int mev_sync_stream_state(const mev_ctx* ctx, const mev_state* st, void* stream);
 
 /* Shared station layout (bs_per_env = 0): (re)derive the association keys the step kernel
  * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the

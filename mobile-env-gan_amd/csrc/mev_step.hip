@@ -579,15 +579,17 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
-  g.s_ok = true;
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue(&at(st.ue_state, 8u * ue));
   if (fused || kp.tab_m) {  // the stream state is read only where a draw needs it (fused:
     g.drawn = kp.tab_m ? at(tb.drawn, 4u * (uint32_t)ec) : 0;  // the caller's LDS slot)
+    // the state row is the stream state without a table, or after draws past it
+    g.s_ok = !kp.tab_m || g.drawn > kp.tab_m;
     g.pa = g.pb = make_ulonglong2(0, 0);
   } else {
     ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
     g.drawn = kp.tab_m ? at(tb.drawn, 4u * (uint32_t)ec) : 0;
+    g.s_ok = true;
     g.pa = at(pr, 48u * (uint32_t)ec);
     g.pb = at(pr, 48u * (uint32_t)ec + 16u);
   }
@@ -799,8 +801,6 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                             : at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)u));
         pos = make_int2((int)(short)p, p >> 16);
         wp = make_int2(-1, -1);
-        if (!FUSED && u == U - 1)
-          s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)u));
       }
     } else if (do_reset) {  // MComCore.reset (base.py:172-209), see k_reset_packed
       const ulonglong2 pc = at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e + 32u);
@@ -844,22 +844,28 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     if (M && (bal(k >= M) & mneed_w) == 0) {
       // draw table: every drawing lane of the wavefront finds its pair precomputed (fused
       // launches read the wavefront's copy in LDS and track only `drawn`)
+      // (the stream state is not written back: with the table it is the entry of pair
+      // drawn - 1 -- see mev.h, mev_state.pcg)
       if (need) {
         const uint32_t row = (uint32_t)e * (uint32_t)M;
         const int p = FUSED ? ltab[m.seg * M + k]
                             : at(const_cast<int*>(tb.tab_xy), 4u * (row + (uint32_t)k));
         wp = make_int2((int)(short)p, p >> 16);
-        if (!FUSED && rank == tot - 1)
-          s_fin = at(const_cast<u128*>(tb.tab_st), 16u * (row + (uint32_t)k));
       }
     } else {
       fell_back = true;
       if (M) {  // beyond the table: from the stream state
-        if (!FUSED) {  // loaded only on this path
+        if (!FUSED) {  // loaded only on this path: the state row holds the stream state only
+          // after draws past the table (drawn > M); before, the table's entry of pair drawn - 1
           ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-          const ulonglong2 pa = at(pr, 48u * (uint32_t)e), pb = at(pr, 48u * (uint32_t)e + 16u);
+          const ulonglong2 pb = at(pr, 48u * (uint32_t)e + 16u);
           inc = mk128(pb.x, pb.y);
-          s = mk128(pa.x, pa.y);
+          if (drawn > 0 && drawn <= M) {
+            s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(drawn - 1)));
+          } else {
+            const ulonglong2 pa = at(pr, 48u * (uint32_t)e);
+            s = mk128(pa.x, pa.y);
+          }
         } else {  // fused: the slot holds the state after a fallback draw, else the table
           inc = slot[1];
           if (!s_ok && drawn > 0) {
@@ -1102,7 +1108,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     store_ue(&at(st.ue_state, 8u * ui), pos, wp);
     at(out.serving, 4u * ui) = srv;
     at(out.obs, 16u * ui) = obs;
-    if (own_fin)  // the stream moved (draws, or reset): write the new state back
+    if (own_fin && (!M || fell_back))  // the stream moved: write the new state back (with the
+                                       // table only after draws past it, mev_state.pcg)
       at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) =
           make_ulonglong2((uint64_t)s_fin, (uint64_t)(s_fin >> 64));
     if (!LEAN && out.rate64) out.rate64[idx] = rate;
@@ -1413,19 +1420,14 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
     if (env_ok && leader) {
       at(st.t, 4u * (uint32_t)e) = a.t;
       if (KPS(tab_m)) at(tb.drawn, 4u * (uint32_t)e) = a.drawn;
-      if (moved) {  // the state after the last pair drawn
-        // (one global load from either the table entry or, without a table, the env's own
-        // state, selected by value: a select of addresses would put a.pa on the stack; the
-        // table index is clamped -- after fallback draws drawn > M, and the entry is unused)
-        ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
-        const ulonglong2 tv =
-            KPS(tab_m) ? at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
-                          16u * ((uint32_t)e * (uint32_t)KPS(tab_m) +
-                                 (uint32_t)max(min(a.drawn, KPS(tab_m)) - 1, 0)))
-                     : at(pcg2, 48u * (uint32_t)e);
+      // the stream state after the last pair drawn, where the slot holds it (without a table:
+      // always; with one: after draws past it -- otherwise the table's entry is the state and
+      // the row is left as it is, mev_state.pcg; no global load, whose wait would drain every
+      // store of the launch)
+      if (moved && a.s_ok) {
         const u128 sl = lpcg[2 * m.seg];
-        const ulonglong2 sf = a.s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
-        at(pcg2, 48u * (uint32_t)e) = sf;
+        at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e) =
+            make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64));
       }
     }
   }
@@ -1740,9 +1742,12 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 
 // The staged rows of k_steps_lds2: reward = (float)isum 2^-25 / nact (float32, as packed_group's
 // lean path), or the utility's lower bound without active UEs; done = bit 7.
+// `trailing`: a second barrier after the reads, before the window's slots are written again
+// (not needed when consecutive pairs alternate between two windows: the next write of this
+// window follows the next flush's first barrier, which every reader here has passed).
 __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
                                               int E, int e0, int row0, int nr, float lower,
-                                              int NWG) {
+                                              int NWG, bool trailing = true) {
   __syncthreads();
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     const int r = q / NWG, j = q - r * NWG;
@@ -1756,7 +1761,82 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
       at(out.done + ro, o) = (uint8_t)(b >> 7);
     }
   }
-  __syncthreads();
+  if (trailing) __syncthreads();
+}
+
+// A pair's inputs (k_steps_lds2), loaded into registers one pair ahead: issued when the wave
+// starts a pair, consumed when it starts the next, so their HBM latency hides behind the
+// current pair's steps. (Loaded at the pair's start instead, every wave of the chip waited for
+// them at the same moment -- the pairs of all waves start together, the workgroup flush being
+// a barrier -- four times per launch, ~3 us each.) Registers, not LDS-DMA: an LDS-DMA in
+// flight makes the compiler wait for it (vmcnt) before every later LDS access of the wave.
+template <int R, int NT>
+struct Pre2 {
+  int2 s[R];    // the lane's UE row {x, y, wx, wy} (int16x4) in each group
+  int td;       // lanes [0, R G): t of env slot `lane`; lanes [R G, 2 R G): drawn of slot lane - R G
+  v4u32 pc;     // lanes [0, 2 R G): {state} (even lane) / {inc} (odd lane) of env slot lane >> 1
+  int tab[NT];  // words q * 64 + lane of the pair's episode draw tables [R G][M]
+};
+
+// Words of the pair's draw tables per lane: R G M / 64 (scenario instances), else at most 8
+// (the host selects k_steps_lds2 only when R G M <= 512).
+template <int UC, int SCN, int R>
+__host__ __device__ constexpr int lds2_pre_words() {
+  return SCN ? (R * (64 / pitch_of(UC)) * scn_const(SCN).tab_m + 63) / 64 : 8;
+}
+
+template <int UC, int SCN, int R, int NT>
+__device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& st,
+                                              const KTables& tb, const LaneMap& m, int lane,
+                                              int p, Pre2<R, NT>& f) {
+  constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC, RG = R * G;
+  const int M = KPS(tab_m);
+  const int e0 = p * RG, elast = kp.E - 1;  // the pair's envs [e0, e0 + R G), clamped
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int ec = min(e0 + r * G + m.seg, elast);
+    f.s[r] = at(st.ue_state, 8u * (uint32_t)(ec * U + min(m.u, U - 1)));
+  }
+  const int ej = min(e0 + (lane < RG ? lane : min(lane - RG, RG - 1)), elast);
+  f.td = at(lane < RG ? st.t : tb.drawn, 4u * (uint32_t)ej);
+  const int ep = min(e0 + min(lane >> 1, RG - 1), elast);
+  f.pc = at(reinterpret_cast<v4u32*>(st.pcg), 48u * (uint32_t)ep + 16u * (uint32_t)(lane & 1));
+  const int lim = max(1, min(RG * M, (kp.E - e0) * M));
+  const int* src = tb.tab_xy + (size_t)e0 * M;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) f.tab[q] = src[min(q * 64 + lane, lim - 1)];
+}
+
+// The prefetched inputs into the pair's contexts and the wave's LDS (draw tables, stream
+// slots; t / drawn through `scratch`, a free histogram area).
+template <int UC, int SCN, int R, int NT>
+__device__ __forceinline__ void lds2_consume(const KParams& kp, const LaneMap& m, int lane, int p,
+                                             const Pre2<R, NT>& f, Ctx2 (&c)[R],
+                                             int* __restrict__ ltab, u128* __restrict__ lpcg,
+                                             int* __restrict__ scratch) {
+  constexpr int PC = pitch_of(UC), G = 64 / PC, RG = R * G;
+  const int M = KPS(tab_m);
+  const int lim = max(1, min(RG * M, (kp.E - p * RG) * M));
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+    if (q * 64 + lane < lim) ltab[q * 64 + lane] = f.tab[q];
+  if (lane < 2 * RG) {
+    reinterpret_cast<v4u32*>(lpcg)[lane] = f.pc;
+    scratch[lane] = f.td;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int slot = r * G + m.seg;
+    c[r].t = scratch[slot];
+    c[r].drawn = scratch[RG + slot];
+    // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
+    c[r].s_ok = c[r].drawn > M;
+    c[r].moved = false;
+    const int2 v = f.s[r];
+    c[r].pos = make_int2((int)(short)v.x, v.x >> 16);
+    c[r].wp = make_int2((int)(short)v.y, v.y >> 16);
+  }
 }
 
 // LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, (PE) station keys [R G][16][2] int,
@@ -1779,14 +1859,6 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC;
   const int NWG = NW * G * R;  // envs per workgroup tile
   extern __shared__ int lds_all[];
-  {  // the tables: LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...
-    const int n16 = KPS(lds_assoc) >> 4;
-    const int ln = threadIdx.x & 63;
-    for (int q = (int)(threadIdx.x >> 6); q * 64 < n16; q += NW)
-      if (q * 64 + ln < n16) glds(tb.lds_blob + q * 64 + ln, reinterpret_cast<int4*>(lds_all) + q * 64);
-    wait_vmem();
-    __syncthreads();
-  }
   const char* lblob = reinterpret_cast<const char*>(lds_all);
   const int M = KPS(tab_m), B = KPS(B);
   const int wv = threadIdx.x >> 6;
@@ -1805,19 +1877,36 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const int npairs = (ngroups + 1) / 2;
   const int gstride = (int)gridDim.x * NW;
   const float lower = (float)kp.lower;
-  for (int pb = block_slot(kp.xcd_remap) * NW; pb < npairs; pb += gstride) {
+  const int pb0 = block_slot(kp.xcd_remap) * NW;
+  constexpr int NT = lds2_pre_words<UC, SCN, R>();
+  Pre2<R, NT> f;  // the inputs of the wave's next pair
+  {  // the tables (LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...) and the first pair's
+     // inputs, issued together before one wait
+    const int n16 = KPS(lds_assoc) >> 4;
+    for (int q = wv; q * 64 < n16; q += NW)
+      if (q * 64 + lane < n16) glds(tb.lds_blob + q * 64 + lane, reinterpret_cast<int4*>(lds_all) + q * 64);
+    if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, NT>(kp, st, tb, m, lane, pb0 + wvu, f);
+    wait_vmem();
+    __syncthreads();
+  }
+  // staged per-env rows: a pair whose steps fit twice in the window alternates between its two
+  // halves (one barrier per flush), else the window cycles (two)
+  const bool alt = 2 * nsteps <= stage_rows;
+  int hb = 0;  // the pair's first row slot (alt)
+  for (int pb = pb0; pb < npairs; pb += gstride, hb = alt ? nsteps - hb : 0) {
     const int p = pb + wvu;
     const int e0 = pb * G * R;  // the workgroup tile's first env
+    int* const sw = srow + hb * NWG;
+    uint8_t* const dw = drow + hb * NWG;
     if (p >= npairs) {  // no pair for this wave: its part of the flushes only
       for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-        flush_staged2(out, srow, drow, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
-                      NWG);
+        flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
+                      NWG, !alt);
       continue;
     }
     Ctx2 c[R];
     int e[R], nok[R];
     bool env_ok[R];
-    ulonglong2 pa[R], pbv[R];
     const bool leader = m.u == PC - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1825,21 +1914,11 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       e[r] = g * G + m.seg;
       env_ok[r] = (m.seg < G) && (e[r] < kp.E);
       nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
-      // the group's draw tables (LDS-DMA) and state, issued before one wait
-      const int nt = G * M;
-      const int lim = max(0, min(nt, (kp.E - g * G) * M));
-      const int* src = tb.tab_xy + (size_t)g * nt;
-      for (int q = 0; q * 64 < lim; ++q)
-        if (q * 64 + lane < lim) glds(src + q * 64 + lane, ltab + r * nt + q * 64);
-      const GroupIn a = load_group(kp, st, tb, e[r], min(m.u, U - 1), U, true);
-      c[r].t = a.t;
-      c[r].drawn = a.drawn;
-      c[r].s_ok = true;
-      c[r].moved = false;
-      c[r].pos = make_int2(a.s.x, a.s.y);
-      c[r].wp = make_int2(a.s.z, a.s.w);
-      pa[r] = pbv[r] = make_ulonglong2(0, 0);
-      if (PE && m.seg < G) {  // the env's station keys (see k_steps_packed's staging)
+    }
+    if (PE) {  // the envs' station keys (see k_steps_packed's staging), before the next pair's
+               // loads are issued (their wait then leaves those in flight)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
         const int ec = min(e[r], kp.E - 1);
         const int nbf = env_ok[r] ? (st.bs_count ? st.bs_count[ec] : B) : 0;
         for (int k = m.u; k < 16; k += PC) {
@@ -1853,31 +1932,20 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           *reinterpret_cast<int2*>(lkeys + (r * G + m.seg) * 32 + 2 * k) = kv;
         }
       }
-      if (env_ok[r] && leader) {
-        ulonglong2* pr = reinterpret_cast<ulonglong2*>(st.pcg);
-        pa[r] = at(pr, 48u * (uint32_t)e[r]);
-        pbv[r] = at(pr, 48u * (uint32_t)e[r] + 16u);
-      }
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (env_ok[r] && leader) {
-        lpcg[2 * (r * G + m.seg)] = mk128(pa[r].x, pa[r].y);
-        lpcg[2 * (r * G + m.seg) + 1] = mk128(pbv[r].x, pbv[r].y);
-      }
-    }
+    lds2_consume<UC, SCN, R, NT>(kp, m, lane, p, f, c, ltab, lpcg, hist);
+    if (p + gstride < npairs) lds2_prefetch<UC, SCN, R, NT>(kp, st, tb, m, lane, p + gstride, f);
     const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
-    __builtin_amdgcn_s_waitcnt(0);
     for (int i = 0, sr = 0; i < nsteps; ++i, sr = sr + 1 == stage_rows ? 0 : sr + 1) {
       lds2_step<UC, SCN, R, PE, TF>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
-                                lblob, lpcg, hist, ltab, srow + sr * NWG + wvu * G * R,
-                                drow + sr * NWG + wvu * G * R, lkeys);
+                                lblob, lpcg, hist, ltab, sw + sr * NWG + wvu * G * R,
+                                dw + sr * NWG + wvu * G * R, lkeys);
       if (sr + 1 == stage_rows || i + 1 == nsteps)
-        flush_staged2(out, srow, drow, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG);
+        flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, !alt);
     }
-    // the state after the last step (see k_steps_packed)
+    // the state after the last step (see k_steps_packed); the stream state only where the slot
+    // holds it (draws past the table, mev_state.pcg): no global load here, whose wait would
+    // drain every store of the pair
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (env_ok[r] && m.u < U)
@@ -1886,15 +1954,10 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       if (env_ok[r] && leader) {
         at(st.t, 4u * (uint32_t)e[r]) = c[r].t;
         at(tb.drawn, 4u * (uint32_t)e[r]) = c[r].drawn;
-        if (mvd) {
-          ulonglong2* pcg2 = reinterpret_cast<ulonglong2*>(st.pcg);
-          const ulonglong2 tv = at(reinterpret_cast<ulonglong2*>(const_cast<u128*>(tb.tab_st)),
-                                   16u * ((uint32_t)e[r] * (uint32_t)M +
-                                          (uint32_t)max(min(c[r].drawn, M) - 1, 0)));
+        if (mvd && c[r].s_ok) {
           const u128 sl = lpcg[2 * (r * G + m.seg)];
-          const ulonglong2 sf =
-              c[r].s_ok ? make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64)) : tv;
-          at(pcg2, 48u * (uint32_t)e[r]) = sf;
+          at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e[r]) =
+              make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64));
         }
       }
     }
@@ -2222,7 +2285,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
     for (int i = u; i < KPS(B); i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
     if (CULL && u == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
-    bool s_ok = true;  // the slot holds the state after the env's last draw
+    // the slot holds the state after the env's last draw: the state row without a table, or
+    // after draws past it (mev_state.pcg)
+    bool s_ok = !M || drawn > M;
     BlockRow prev{0, 0, 0};
     // step 0's per-wave need / active counts (its lazy reset applied ahead)
     auto ahead_counts = [&](int tn, int2 wpn, int* wt) {
@@ -2538,9 +2603,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     if (u == 0) {
       st.t[e] = t;
       if (M) tb.drawn[e] = drawn;
-      const u128 sf = (s_ok || !M) ? L.slot[0] : tb.tab_st[(size_t)e * M + (min(drawn, M) - 1)];
-      *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
-          make_ulonglong2((uint64_t)sf, (uint64_t)(sf >> 64));
+      if (s_ok || !M) {  // (with a table and drawn <= M its entry is the state: row unchanged)
+        const u128 sf = L.slot[0];
+        *reinterpret_cast<ulonglong2*>(st.pcg + (size_t)6 * e) =
+            make_ulonglong2((uint64_t)sf, (uint64_t)(sf >> 64));
+      }
     }
     __syncthreads();  // LDS reused by the next env
   }
@@ -2715,6 +2782,18 @@ __global__ void k_draw_table(KParams kp, const uint64_t* __restrict__ pcg,
                                 x, y);
   tab_xy[i] = (int)(((unsigned)x & 0xffffu) | ((unsigned)y << 16));
   tab_st[i] = s2;
+}
+
+// The stream state after the env's draws so far into its pcg row, where the kernels left it
+// to the draw table (drawn in [1, M]: the state is the table's entry of pair drawn - 1).
+__global__ void k_sync_stream_state(int E, int M, const int* __restrict__ drawn,
+                                    const u128* __restrict__ tab_st, uint64_t* __restrict__ pcg) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int d = drawn[e];
+  if (d < 1 || d > M) return;
+  const u128 s = tab_st[(size_t)e * M + (d - 1)];
+  *reinterpret_cast<ulonglong2*>(pcg + (size_t)6 * e) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
 }
 
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
@@ -3616,7 +3695,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const int ldsm = ldsa ? kp.lds_mode : 0;
     // two env groups per wavefront when the batch fills every resident workgroup with them
     const int pairs = (groups + 1) / 2;
-    if (c->p.bs_per_env && kp.lds_mode == 4 && lean && traj && c->lds2_wgs > 0 &&
+    // (k_steps_lds2 prefetches a pair's draw tables into at most 8 registers per lane)
+    const bool pre_ok = 2 * kp.envs_per_wave * kp.tab_m <= 64 * lds2_pre_words<30, 0, 2>();
+    if (c->p.bs_per_env && kp.lds_mode == 4 && lean && traj && c->lds2_wgs > 0 && pre_ok &&
         pairs >= c->lds2_wgs * kLds2Waves) {  // per-env layouts (k_steps_lds2<U, 0, true>)
       StepsKernel k2 = kp.U == 15 ? k_steps_lds2<15, 0, true>
                                   : (match_scn(c) == 3 ? (c->tie_free ? k_steps_lds2<30, 3, true, true>
@@ -3633,7 +3714,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       MEV_HIP(hipGetLastError());
       return MEV_OK;
     }
-    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pairs >= c->lds2_wgs * kLds2Waves) {
+    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && pairs >= c->lds2_wgs * kLds2Waves) {
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
       StepsKernel k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true>
@@ -3794,6 +3875,15 @@ int mev_prepare_draws(const mev_ctx* c, const mev_state* st, const uint8_t* env_
   hipLaunchKernelGGL(k_draw_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, c->kp, st->pcg, env_mask, c->jump, c->tab_xy,
                      c->tab_st);
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
+int mev_sync_stream_state(const mev_ctx* c, const mev_state* st, void* stream) {
+  if (!c || !st || !st->pcg) return MEV_EINVAL;
+  if (!c->kp.tab_m) return MEV_OK;  // without the table the rows are always current
+  hipLaunchKernelGGL(k_sync_stream_state, dim3((unsigned)((c->kp.E + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, c->kp.E, c->kp.tab_m, c->drawn, c->tab_st, st->pcg);
   MEV_HIP(hipGetLastError());
   return MEV_OK;
 }

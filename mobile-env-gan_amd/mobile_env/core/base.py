@@ -144,6 +144,7 @@ class MComCore:
             return self._engine
         carry = None
         if self._engine is not None:  # new layout (MComCustom): keep the movement stream
+            self._engine.sync_stream_state()
             carry = (self._engine.pcg.clone(), self._engine.t.clone())
             self._engine.close()
         p = lowering.lower(num_envs=1, stations=stations, users=users,

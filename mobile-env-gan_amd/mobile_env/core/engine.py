@@ -343,6 +343,14 @@ class StepEngine:
             N.check(self._lib.mev_prepare_draws(self._ctx, C.byref(self._st), None,
                                                 self._stream()), "mev_prepare_draws")
 
+    def sync_stream_state(self):
+        """Materialise every env's movement stream state in ``pcg`` (mev_sync_stream_state):
+        with the episode draw table the kernels leave the state column as it is while an
+        episode's draws stay inside the table. Call before reading or saving ``pcg``."""
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_sync_stream_state(self._ctx, C.byref(self._st), self._stream()),
+                    "mev_sync_stream_state")
+
     def set_bs_layout(self, bs_xy, bs_count=None):
         bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)
         if tuple(bs.shape) != tuple(self.bs_xy.shape):

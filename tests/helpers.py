@@ -52,3 +52,11 @@ def make_engine(d, device="cuda", bs=None, ue=None, stream_split=0, draw_table=-
                      stream_split=stream_split, draw_table=draw_table,
                      fuse_steps=fuse_steps)
     return StepEngine(p, bs_xy, d["seeds"], bs_count=cnt, device=device, **kw)
+
+
+def synced_pcg(eng):
+    """The engine's pcg rows with every stream state materialised (mev_sync_stream_state: the
+    kernels leave the state column to the draw table while an episode's draws stay inside it),
+    so launch shapes with and without the table compare equal."""
+    eng.sync_stream_state()
+    return eng.pcg
