@@ -40,6 +40,7 @@ class OracleParams:
     lower: float = -20             # base.py:136
     upper: float = 20
     coeffs: tuple = (10, 0, 10)
+    movement_reseed: bool = True   # movement_params reset_rng_episode (base.py:133, movement.py:16-18)
     # heterogeneous entities (entities.py:7-22,33-45): per-station / per-UE parameter classes
     # ({bw, freq, tx, height} / {velocity, snr_tr, noise, height}) and each entity's class
     bs_classes: list = None
@@ -135,8 +136,11 @@ class OracleBatch:
         envs = range(self.E) if envs is None else envs
         W, H = self.p.width, self.p.height
         for e in envs:
-            # movement seed = config seed + 4 (base.py:156-168); re-seeded every episode
-            g = np.random.default_rng(int(self.seeds[e]) + 4)
+            # movement seed = config seed + 4 (base.py:156-168); re-seeded every episode when
+            # reset_rng_episode (the default), else created once and continued (movement.py:16-18)
+            g = self.gens[e]
+            if self.p.movement_reseed or g is None:
+                g = np.random.default_rng(int(self.seeds[e]) + 4)
             self.gens[e] = g
             for u in range(self.U):
                 self.x[e, u] = int(g.uniform(0, W))

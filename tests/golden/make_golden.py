@@ -13,7 +13,7 @@ stub modules for its render-only / geometry dependencies that are absent from th
 * ``svgpath2mpl``       -- BS glyph for rendering only (reference util.py:4,24)
 
 The per-step JSON dump of the reference (base.py:261,298-349) is disabled and the process runs
-from a scratch directory. Usage:  python tests/golden/make_golden.py [--extra]
+from a scratch directory. Usage:  python tests/golden/make_golden.py [--extra | --knobs]
 """
 from __future__ import annotations
 
@@ -245,6 +245,83 @@ def extra_fixtures(ref_base, BaseStation, UserEquipment):
     return out
 
 
+def run_until_done(env, users, episodes):
+    """The driver loop with the episode ending where the reference says it does:
+    reset(); step() while not time_is_up (base.py:407-409: time >= min(EP_MAX_TIME,
+    max_departure))."""
+    rec = {k: [] for k in ("init_xy", "xy", "serving", "rate", "util", "metrics")}
+    lens = []
+    for ep in range(episodes):
+        env.reset()
+        rec["init_xy"].append([[int(ue.x), int(ue.y)] for ue in users])
+        s = 0
+        while not env.time_is_up:
+            env.step(ep, s)
+            xy, srv, rate, util, met = _record_step(env, users)
+            for k, v in zip(("xy", "serving", "rate", "util", "metrics"), (xy, srv, rate, util, met)):
+                rec[k].append(v)
+            s += 1
+        lens.append(s)
+    out = {k: np.asarray(v) for k, v in rec.items()}
+    out["episode_len"] = np.asarray(lens)
+    return out
+
+
+# Reference config knobs the engine lowers into kernel branches (MComCore.default_config,
+# base.py:103-153, deep-merged at base.py:47): name -> (layout, num_ues, velocity, seeds,
+# episodes, config overrides). "block" variants use 96 UEs (U > 64: the one-workgroup-per-env
+# kernel).
+KNOBS = {
+    "knob_noreseed_large": ("large", None, None, [2024, 99], 3,
+                            {"movement_params": {"reset_rng_episode": False}}),
+    "knob_noreseed_small_v10": ("small", None, 10, [5, 2024], 3,
+                                {"movement_params": {"reset_rng_episode": False}}),
+    "knob_ept12_large": ("large", None, None, [2024, 7], 3, {"EP_MAX_TIME": 12}),
+    "knob_ept30_medium": ("medium", None, None, [2024, 11], 2, {"EP_MAX_TIME": 30}),
+    "knob_ep15_medium_v10": ("medium", None, 10, [3, 2024], 3,
+                             {"arrival_params": {"ep_time": 15}}),
+    "knob_util_large_v10": ("large", None, 10, [2024, 31], 2,
+                            {"utility_params": {"lower": -10, "upper": 15, "coeffs": (5, 1, 2)}}),
+    "knob_block_noreseed": ("large", 96, 10, [2024, 8], 3,
+                            {"movement_params": {"reset_rng_episode": False}}),
+    "knob_block_ept12": ("large", 96, 10, [2024], 3, {"EP_MAX_TIME": 12}),
+    "knob_block_util": ("large", 96, 10, [17], 2,
+                        {"utility_params": {"lower": -10, "upper": 15, "coeffs": (5, 1, 2)}}),
+}
+
+
+def knob_fixtures(ref_base, BaseStation, UserEquipment):
+    build = _make_fixed_core(ref_base, BaseStation, UserEquipment)
+    layouts = json.load(open(LAYOUTS))
+    defaults = ref_base.MComCore.default_config()
+    out = {}
+    for name, (lay_name, nue, vel, seeds, episodes, cfg) in KNOBS.items():
+        lay = layouts[lay_name]
+        U = nue or lay["num_ues"]
+        runs = []
+        for seed in seeds:
+            env, users = build(lay["bs"], U, seed,
+                               ue_params={"velocity": vel} if vel is not None else None,
+                               extra=json.loads(json.dumps(cfg)))
+            runs.append(run_until_done(env, users, episodes))
+        out[name] = dict(
+            bs_xy=np.asarray(lay["bs"], dtype=np.int64), seeds=np.asarray(seeds, dtype=np.int64),
+            velocity=np.float64(vel if vel is not None else defaults["ue"]["velocity"]),
+            config=json.dumps(cfg),
+            **{k: np.stack([r[k] for r in runs]) for k in runs[0]})
+        print(name, "episode lengths", runs[0]["episode_len"].tolist())
+    return out
+
+
+def main_knobs():
+    ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
+    scratch = tempfile.mkdtemp(prefix="mev_golden_")
+    os.chdir(scratch)
+    for name, arrs in knob_fixtures(ref_base, BaseStation, UserEquipment).items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+        print("wrote", name)
+
+
 def main_extra():
     ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
     scratch = tempfile.mkdtemp(prefix="mev_golden_")
@@ -370,5 +447,11 @@ def main():
 
 
 if __name__ == "__main__":
-    # --extra: only the round-2 fixtures (per-env 128 x 1024, heterogeneous parameters)
-    main_extra() if "--extra" in sys.argv[1:] else main()
+    # --extra: only the round-2 fixtures (per-env 128 x 1024, heterogeneous parameters);
+    # --knobs: only the round-3 config-knob fixtures (KNOBS)
+    if "--extra" in sys.argv[1:]:
+        main_extra()
+    elif "--knobs" in sys.argv[1:]:
+        main_knobs()
+    else:
+        main()

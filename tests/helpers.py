@@ -14,6 +14,10 @@ DEFAULT_UE = {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
 # fixture name -> (num_ues, per-env ragged layout?)
 FIXTURES = ("small", "medium", "large", "small_v10", "large_v10", "mcom_custom",
             "custom128x1024", "custom128x1024_perenv")
+# reference config knobs (tests/golden/make_golden.py --knobs: KNOBS)
+KNOB_FIXTURES = ("knob_noreseed_large", "knob_noreseed_small_v10", "knob_ept12_large",
+                 "knob_ept30_medium", "knob_ep15_medium_v10", "knob_util_large_v10",
+                 "knob_block_noreseed", "knob_block_ept12", "knob_block_util")
 
 
 def load(name):
@@ -60,3 +64,69 @@ def synced_pcg(eng):
     so launch shapes with and without the table compare equal."""
     eng.sync_stream_state()
     return eng.pcg
+
+
+def knob_config(d):
+    """The reference config overrides a knob fixture was generated with."""
+    return json.loads(str(d["config"]))
+
+
+def knob_oracle_params(d):
+    """OracleParams of a knob fixture, read from its reference config dict (the keys of
+    MComCore.default_config, base.py:103-153)."""
+    from oracle.vec import OracleParams
+    cfg = knob_config(d)
+    up = cfg.get("utility_params", {})
+    return OracleParams(
+        velocity=float(d["velocity"]), ep_max_time=int(cfg.get("EP_MAX_TIME", 20)),
+        arrival_ep_time=int(cfg.get("arrival_params", {}).get("ep_time", 20)),
+        lower=up.get("lower", -20), upper=up.get("upper", 20),
+        coeffs=tuple(up.get("coeffs", (10, 0, 10))),
+        movement_reseed=bool(cfg.get("movement_params", {}).get("reset_rng_episode", True)))
+
+
+def knob_params(d, num_envs=None):
+    """EngineParams of a knob fixture lowered the way the facade lowers a reference config:
+    MComCore(stations, users, config) (deep merge into default_config, plugin objects built
+    from config[k] / config[k + "_params"], base.py:47-61) -> lowering.lower. The episode draw
+    table is left automatic (the facade itself turns it off)."""
+    from mobile_env.core import lowering
+    from mobile_env.core.base import MComCore
+    from mobile_env.core.entities import BaseStation, UserEquipment
+    base = MComCore.default_config()
+    U = d["xy"].shape[-2]
+    stations = [BaseStation(i, (int(x), int(y)), **base["bs"])
+                for i, (x, y) in enumerate(d["bs_xy"])]
+    users = [UserEquipment(i, **dict(base["ue"], velocity=float(d["velocity"])))
+             for i in range(U)]
+    core = MComCore(stations, users, config=knob_config(d))
+    p = lowering.lower(num_envs=num_envs or len(d["seeds"]), stations=stations, users=users,
+                       arrival=core.arrivalModel, channel=core.channelModel,
+                       scheduler=core.schedulerModel, movement=core.movementModel,
+                       utility=core.utilityModel, ep_max_time=core.EP_MAX_TIME,
+                       first_step_active=True)
+    p.draw_table = -1
+    return p
+
+
+def knob_engine(d, num_envs=None, device="cuda", rate64=False, util64=False, metrics=False,
+                **launch):
+    """StepEngine over a knob fixture: env i runs the fixture's seed i % n (replicas give
+    batch sizes that select the large-batch kernels); `launch` sets EngineParams fields."""
+    from mobile_env.core.engine import StepEngine
+    p = knob_params(d, num_envs)
+    for k, v in launch.items():
+        setattr(p, k, v)
+    E = p.num_envs
+    seeds = np.asarray(d["seeds"])[np.arange(E) % len(d["seeds"])]
+    return StepEngine(p, d["bs_xy"], seeds, device=device, rate64=rate64, util64=util64,
+                      metrics=metrics)
+
+
+def knob_done(d):
+    """done flag of every fixture step (the last step of each episode)."""
+    lens = np.asarray(d["episode_len"])[0]
+    ends = np.cumsum(lens) - 1
+    done = np.zeros(int(lens.sum()), dtype=bool)
+    done[ends] = True
+    return done

@@ -174,3 +174,40 @@ def test_mcom_core_facade_heterogeneous_entities():
                 assert rates == d["rate"][k, ep * 20 + s].tolist()
         assert env.check_connectivity(st[0], us[0]) in (True, False)
         env.close()
+
+
+@pytest.mark.parametrize("which", ["default", "notebook"])
+def test_c_caller_libm_table_shares_round_like_reference(golden_dir, which):
+    """A C caller that passes no rate table (mev_params.rate_table = NULL) gets mev_create's libm
+    table; the rounded ResourceFair shares the kernels form from it (both device paths: the
+    reciprocal form for every n <= 1024, the 100/n table form for n <= 64) equal the
+    reference's numpy round(rate / n, 2) (base.py:427-435) on the reference's own rates."""
+    import ctypes as C
+    import json
+
+    import torch
+    from mobile_env.core import _native as N
+    from mobile_env.core.engine import EngineParams
+    c = np.load(f"{golden_dir}/channel_{which}.npz")
+    bs, ue = json.loads(str(c["bs"])), json.loads(str(c["ue"]))
+    cp = EngineParams(num_envs=1, num_ues=1024, num_bs=3, bs=bs,
+                      ue={k: ue[k] for k in ("snr_tr", "noise", "height")}).to_c(False)
+    assert not cp.rate_table  # the C library builds the table
+    L = N.lib()
+    ctx = C.c_void_p()
+    with torch.cuda.device(0):
+        N.check(L.mev_create(C.byref(cp), C.byref(ctx)), "mev_create")
+        try:
+            assert L.mev_d2max(ctx) == int(c["d2max"])
+            ref = c["rate"]
+            for path, nmax in ((0, 1024), (1, 64)):
+                out = torch.empty((nmax, len(ref)), dtype=torch.float64, device="cuda")
+                N.check(L.mev_share_cents(ctx, nmax, path, C.c_void_p(out.data_ptr()), None),
+                        "mev_share_cents")
+                torch.cuda.synchronize()
+                got = out.cpu().numpy()
+                for n in range(1, nmax + 1):
+                    np.testing.assert_array_equal(got[n - 1] / 100.0, np.round(ref / n, 2),
+                                                  err_msg=f"path {path} share count {n}")
+        finally:
+            L.mev_destroy(ctx)

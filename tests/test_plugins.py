@@ -51,6 +51,32 @@ def test_c_library_table_within_a_few_ulp(golden_dir):
     assert ulps.max() <= 4 and (ulps != 0).mean() < 0.01
 
 
+@pytest.mark.parametrize("which", ["default", "notebook"])
+def test_c_library_table_rounds_like_the_reference(golden_dir, which):
+    """What a C caller of the libm table (mev_params.rate_table = NULL) depends on: the
+    ResourceFair share rounded to cents, numpy round(rate / n, 2) (base.py:427-435), equals the
+    reference's for every connectable d2 and every share count n <= 1024 (the largest U), on
+    both channel parameter sets -- the few entries that differ by an ulp or two never move a
+    cent."""
+    import ctypes as C
+    from mobile_env.core import _native as N
+    from mobile_env.core.engine import EngineParams
+    c = np.load(f"{golden_dir}/channel_{which}.npz")
+    bs, ue = json.loads(str(c["bs"])), json.loads(str(c["ue"]))
+    cp = EngineParams(num_envs=1, num_ues=5, num_bs=3, bs=bs,
+                      ue={k: ue[k] for k in ("snr_tr", "noise", "height")}).to_c(False)
+    lib = N.lib()
+    n = lib.mev_build_rate_table(C.byref(cp), None, 0)
+    assert n == int(c["d2max"]) + 1
+    tab = np.zeros(n)
+    assert lib.mev_build_rate_table(C.byref(cp), tab.ctypes.data, n) == n
+    ref = c["rate"]
+    assert (tab != ref).any() or which == "notebook"  # (the default table has differing entries)
+    for k in range(1, 1025):
+        np.testing.assert_array_equal(np.round(tab / k, 2), np.round(ref / k, 2),
+                                      err_msg=f"share count {k}")
+
+
 def test_channel_methods_match_reference_table(golden_dir):
     """Channel.calculateSNR / datarate + OkumuraHata.power_loss on entity pairs at integer
     squared distances d2 equal the reference's table entry (channels.py:24-27,78-83,133-146),
