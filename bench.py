@@ -39,6 +39,13 @@ Contract (see DESIGN.md "Measurement"):
 * cpu_baseline (rank 0, N = 1): the per-object CPU port of the reference step (oracle/port.py,
   bit-exact vs the reference fixtures) on a bounded sample of the same workload, one process
   per core of the host share, run before the GPU is touched.
+* N > 1 without a launcher (``python bench.py --gpus N``, WORLD_SIZE unset): this process starts
+  the N rank processes itself (torch.distributed.run on 127.0.0.1, a free port) before it touches
+  the GPU, and exits with their exit code; each rank runs the contract above. The line reports
+  the world size and backend the ranks saw, and (outside the step timing) the north-star final
+  obs all-gather over RCCL (mobile_env.sharding.gather_obs): its time and bytes.
+* --stub-engine: a CPU stand-in engine with the gloo backend (tests of the launcher, sharding and
+  timing glue on a machine without a GPU; never a measurement).
 """
 from __future__ import annotations
 
@@ -196,6 +203,70 @@ def roofline(algo_bytes, launch_ms, traffic):
             "algorithmic_bytes_per_launch": algo_bytes, "launch_ms": launch_ms}
 
 
+class StubEnv:
+    """CPU stand-in for the GPU engine (--stub-engine; tests only): after k steps every env's
+    reward is its config seed + k, done = (k % 20 == 0) and its obs rows hold the seed -- so a
+    gathered batch is checkable."""
+    bs_per_env = False
+    launch_parts = 1
+    fused_steps = True
+
+    def __init__(self, num_envs, num_ues, num_bs, seeds):
+        import torch
+        self.engine = self
+        self.num_ues, self.num_bs = num_ues, num_bs
+        self.seeds = torch.as_tensor(seeds, dtype=torch.float32)
+        self.k = 0
+        self.obs = torch.zeros((num_envs, num_ues, 4))
+        self.reward = torch.zeros(num_envs)
+        self.done = torch.zeros(num_envs, dtype=torch.uint8)
+
+    def trajectory(self, n):
+        import types
+        import torch
+        E, U = self.obs.shape[:2]
+        return types.SimpleNamespace(obs=torch.zeros((n, E, U, 4)), reward=torch.zeros((n, E)),
+                                     done=torch.zeros((n, E), dtype=torch.uint8))
+
+    def launcher(self, n, traj=None):
+        def go():
+            for i in range(n):
+                self.k += 1
+                r, d = self.seeds + self.k, int(self.k % 20 == 0)
+                o, rw, dn = ((traj.obs[i], traj.reward[i], traj.done[i]) if traj is not None
+                             else (self.obs, self.reward, self.done))
+                o.copy_(self.seeds[:, None, None].expand_as(o))
+                rw.copy_(r)
+                dn.fill_(d)
+        return go
+
+    def reset(self):
+        self.k = 0
+
+    def step(self):
+        self.launcher(1)()
+
+    def close(self):
+        pass
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``bench.py --gpus N`` without a launcher: start the N ranks under torch.distributed.run
+    (127.0.0.1, a free port) and return their exit code. This process has not touched the GPU
+    (nothing before this point initialises HIP), so starting fresh processes is safe."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__),
+           *argv]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,45 +294,62 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no step roofline)")
+    ap.add_argument("--stub-engine", action="store_true",
+                    help="CPU stand-in engine + gloo (tests of the multi-rank glue; no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # no launcher: start the ranks
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    stub = args.stub_engine
 
     cpu = None
-    if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.profile_run):
+    if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.profile_run or stub):
         cpu = cpu_baseline(args.cpu_budget, host_share_cores(), args.workload)
 
     import torch
     import torch.distributed as dist
 
-    import mobile_env
-
     # one process per GPU over RCCL; on a box with fewer GPUs than ranks (rehearsal only) the
     # ranks share devices and fall back to gloo (RCCL refuses two ranks on one GPU)
-    ndev = max(1, torch.cuda.device_count())
-    device = torch.device("cuda", local_rank % ndev)
-    torch.cuda.set_device(device)
+    if stub:
+        device, ndev = torch.device("cpu"), 0
+    else:
+        ndev = max(1, torch.cuda.device_count())
+        device = torch.device("cuda", local_rank % ndev)
+        torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("MEV_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
+        backend = "gloo" if stub else os.environ.get("MEV_DIST_BACKEND",
+                                                     "nccl" if ndev >= world else "gloo")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
 
-    from mobile_env.sharding import gather_final, shard_seeds
+    from mobile_env.sharding import gather_final, gather_obs, shard_seeds
 
     E = args.envs
     seeds = shard_seeds(1000, E, rank)  # rank r owns global envs [r*E, (r+1)*E)
     overrides = {k: int(v) for k, v in (kv.split("=", 1) for kv in args.engine)}
-    env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
-                          stream_split=2 if args.launch == "split" else 0,
-                          fuse_steps=0 if args.launch == "fused" else -1, **overrides)
+    if stub:
+        from mobile_env.scenarios import registry
+        sp = registry.spec(args.workload)
+        env = StubEnv(E, sp["num_ues"], sp["num_bs"], seeds)
+    else:
+        import mobile_env
+        env = mobile_env.make(args.workload, num_envs=E, device=device, seed=int(seeds[0]),
+                              stream_split=2 if args.launch == "split" else 0,
+                              fuse_steps=0 if args.launch == "fused" else -1, **overrides)
     eng = env.engine
+
+    def sync():
+        if not stub:
+            torch.cuda.synchronize(device)
     U, B = env.num_ues, env.num_bs
     per_env_bs = eng.bs_per_env
     parts = eng.launch_parts
@@ -271,7 +359,7 @@ def main():
     CHUNK = plan[0]
     fused = args.launch == "fused" and eng.fused_steps
     traj = eng.trajectory(CHUNK) if args.launch == "fused" else None
-    stream = torch.cuda.current_stream(device)
+    stream = None if stub else torch.cuda.current_stream(device)
 
     launchers = {}
 
@@ -289,13 +377,13 @@ def main():
         for n in chunk_plan(args.warmup - 1, CHUNK) if args.warmup > 1 else []:
             issue(n)
             warm += n
-        torch.cuda.synchronize(device)
+        sync()
         while time.perf_counter() - t_w < args.warmup_floor_s:
             for _ in range(16):
                 issue(CHUNK)
                 warm += CHUNK
-            torch.cuda.synchronize(device)
-    torch.cuda.synchronize(device)
+            sync()
+    sync()
 
     class _Ev:
         def __init__(self):  # recorded once here: the HIP event exists before the timed region
@@ -305,26 +393,59 @@ def main():
         def record(self):
             self.e.record(stream)
 
+    class _WallEv:  # (stub engine: host clock)
+        def __init__(self):
+            self.t = time.perf_counter()
+
+        def record(self):
+            self.t = time.perf_counter()
+
+        @property
+        def e(self):
+            return self
+
+        def elapsed_time(self, other):
+            return (other.t - self.t) * 1e3
+
+    gathered = {}
+
     def collective():
         if world > 1:  # the one collective: final (reward, done) batch to every rank
             if traj is not None:  # the last step's row of the trajectory
-                gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
+                gathered["rd"] = gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
             else:
-                gather_final(eng.reward, eng.done)
+                gathered["rd"] = gather_final(eng.reward, eng.done)
 
     for n in set(plan):  # every launch of the timed region prebuilt
         if n not in launchers:
             launchers[n] = eng.launcher(n, traj)
     barrier = dist.barrier if world > 1 else (lambda: None)
-    elapsed, events = timed_run(issue, plan, lambda: torch.cuda.synchronize(device), barrier,
-                                _Ev, collective)
+    elapsed, events = timed_run(issue, plan, sync, barrier, _WallEv if stub else _Ev, collective)
     elapsed = max_over_ranks(elapsed, device)
+
+    # after the timed region: the north-star final obs batch to every rank (RCCL all-gather over
+    # xGMI; obs of the last step), timed on its own (barrier + sync around, max over ranks)
+    obs_gather = None
+    if world > 1:
+        obs_last = traj.obs[plan[-1] - 1] if traj is not None else eng.obs
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        g_obs = gather_obs(obs_last)
+        sync()
+        ms = max_over_ranks((time.perf_counter() - t0) * 1e3, device)
+        nbytes = obs_last.numel() * obs_last.element_size()
+        obs_gather = {"ms": ms, "bytes_per_rank": nbytes, "gathered_bytes": world * nbytes,
+                      "shape": list(g_obs.shape), "backend": dist.get_backend(),
+                      "bus_GBps": (world - 1) * nbytes / (ms * 1e-3) / 1e9,
+                      "checksum": float(g_obs[..., 0].double().sum())}
+        del g_obs
     # the launch shape's average duration over the full-size launches (events on the stream)
     full = [a.e.elapsed_time(b.e) for a, b, n in events if n == CHUNK]
     chunk_ms = sum(full) / len(full)
 
     step_roof = None
-    if rank == 0 and fused and not args.profile_run and args.step_launches > 0:
+    if rank == 0 and fused and not args.profile_run and args.step_launches > 0 and not stub:
         # the Gym step() launch (mev_step(1)), canonical bytes, timed after the timed region:
         # back-to-back launches between one event pair (an event pair around every launch
         # adds ~2 us of marker overhead to a 19 us kernel), in 10 groups for the spread
@@ -394,7 +515,16 @@ def main():
             "roofline": roof,
             "roofline_step": step_roof,
             "cpu_baseline": cpu,
+            "distributed": ({"world_size_seen": dist.get_world_size(),
+                             "backend": dist.get_backend(),
+                             "final_batch": {"shape": list(gathered["rd"].shape),
+                                             "reward_sum": float(gathered["rd"][:, 0].double().sum()),
+                                             "done_sum": float(gathered["rd"][:, 1].double().sum())},
+                             "obs_gather": obs_gather}
+                            if world > 1 else None),
         }
+        if stub:
+            out["data"] = "STUB ENGINE (CPU stand-in, glue test only; not a measurement)"
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:

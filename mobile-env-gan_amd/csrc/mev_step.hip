@@ -649,6 +649,7 @@ struct Pending {
 };
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 
 // s_waitcnt vmcnt(0) only (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait on those)
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
@@ -1742,13 +1743,24 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 
 // The staged rows of k_steps_lds2: reward = (float)isum 2^-25 / nact (float32, as packed_group's
 // lean path), or the utility's lower bound without active UEs; done = bit 7.
+// Workgroup barrier for LDS data: this wave's LDS operations complete (lgkmcnt(0)), then
+// s_barrier; compiler-only fences keep the LDS accesses on their side. Unlike __syncthreads no
+// memory-model fence: its release could also wait for the wave's global stores in flight
+// (vmcnt(0), seen in the generated code), a drain of the trajectory stores at every flush.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only (vmcnt 63, expcnt 7: no wait)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
 __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
                                               int E, int e0, int row0, int nr, float lower,
                                               int NWG, bool trailing = true) {
-  __syncthreads();
+  lds_barrier();
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     const int r = q / NWG, j = q - r * NWG;
     if (e0 + j < E) {
@@ -1761,8 +1773,23 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
       at(out.done + ro, o) = (uint8_t)(b >> 7);
     }
   }
-  if (trailing) __syncthreads();
+  if (trailing) lds_barrier();
 }
+
+// Dev builds only (-DMEV_TIMING, tools/ts_probe.py): per-wave timestamps of k_steps_lds2's
+// phases (s_memrealtime, 100 MHz) into a buffer set by mev_debug_timestamps.
+#ifdef MEV_TIMING
+__device__ uint64_t* g_mev_ts;
+#define MEV_TS(k)                                                                         \
+  do {                                                                                    \
+    if (g_mev_ts && lane == 0)                                                            \
+      g_mev_ts[(size_t)(blockIdx.x * NW + wv) * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MEV_TS(k) \
+  do {            \
+  } while (0)
+#endif
 
 // A pair's inputs (k_steps_lds2), loaded into registers one pair ahead: issued when the wave
 // starts a pair, consumed when it starts the next, so their HBM latency hides behind the
@@ -1770,12 +1797,14 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
 // them at the same moment -- the pairs of all waves start together, the workgroup flush being
 // a barrier -- four times per launch, ~3 us each.) Registers, not LDS-DMA: an LDS-DMA in
 // flight makes the compiler wait for it (vmcnt) before every later LDS access of the wave.
-template <int R, int NT>
+template <int R, int NT, int NK>
 struct Pre2 {
-  int2 s[R];    // the lane's UE row {x, y, wx, wy} (int16x4) in each group
-  int td;       // lanes [0, R G): t of env slot `lane`; lanes [R G, 2 R G): drawn of slot lane - R G
-  v4u32 pc;     // lanes [0, 2 R G): {state} (even lane) / {inc} (odd lane) of env slot lane >> 1
+  v2u32 s[R];   // the lane's UE row {x, y, wx, wy} (int16x4) in each group
+  int t, d, c;  // lanes [0, R G): t, drawn and (per-env layouts) the station count of env slot
+                // `lane` (each from a wave-uniform base: no per-lane pointer kept live)
+  v2u32 pc;     // lanes [0, 4 R G): word lane & 3 of {state, inc} of env slot lane >> 2
   int tab[NT];  // words q * 64 + lane of the pair's episode draw tables [R G][M]
+  v2u32 bq[NK]; // (per-env layouts) station (slot, k) = (i >> 4, i & 15), i = q * 64 + lane
 };
 
 // Words of the pair's draw tables per lane: R G M / 64 (scenario instances), else at most 8
@@ -1785,46 +1814,120 @@ __host__ __device__ constexpr int lds2_pre_words() {
   return SCN ? (R * (64 / pitch_of(UC)) * scn_const(SCN).tab_m + 63) / 64 : 8;
 }
 
-template <int UC, int SCN, int R, int NT>
+// The prefetch loads are inline assembly, i.e. invisible to the compiler's wait-count
+// bookkeeping: tracked, their use one pair later got a compiler wait counted from the shortest
+// path (one step), vmcnt(~18) -- and since vmcnt retires loads and stores in issue order, that
+// waited for every trajectory store more than ~18 instructions back, ~5 us at each pair
+// boundary of a write-bound launch (tools/ts_probe.py). lds2_consume waits for them explicitly
+// (lds2_pf_wait): after >= 63 younger VMEM instructions (nsteps >= 14: four unconditional
+// trajectory stores per step, eight state stores per pair) vmcnt(63) -- which only waits for
+// instructions at least 63 back, and the counter never exceeds 63 -- else vmcnt(0). The
+// registers stay untouched in between (tied to the wait by "+v"; checked on the generated
+// assembly by tools/check_prefetch_regs.py: no copy, no spill).
+__device__ __forceinline__ int pf_b32(const void* p) {
+  int v;
+  asm volatile("global_load_dword %0, %1, off ; mev-prefetch" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ v2u32 pf_b64(const void* p) {
+  v2u32 v;
+  asm volatile("global_load_dwordx2 %0, %1, off ; mev-prefetch" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void pf_tie(T& x) {
+  asm volatile("; mev-prefetch-wait %0" : "+v"(x));
+}
+template <int R, int NT, int NK, bool PE>
+__device__ __forceinline__ void lds2_pf_wait(Pre2<R, NT, NK>& f, bool saturated) {
+  if (saturated) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < R; ++r) pf_tie(f.s[r]);
+  pf_tie(f.t);
+  pf_tie(f.d);
+  if (PE) pf_tie(f.c);
+  pf_tie(f.pc);
+#pragma unroll
+  for (int q = 0; q < NT; ++q) pf_tie(f.tab[q]);
+  if (PE) {
+#pragma unroll
+    for (int q = 0; q < NK; ++q) pf_tie(f.bq[q]);
+  }
+}
+
+template <int UC, int SCN, int R, bool PE, int NT, int NK>
 __device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& st,
                                               const KTables& tb, const LaneMap& m, int lane,
-                                              int p, Pre2<R, NT>& f) {
+                                              int p, Pre2<R, NT, NK>& f) {
   constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC, RG = R * G;
   const int M = KPS(tab_m);
   const int e0 = p * RG, elast = kp.E - 1;  // the pair's envs [e0, e0 + R G), clamped
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int ec = min(e0 + r * G + m.seg, elast);
-    f.s[r] = at(st.ue_state, 8u * (uint32_t)(ec * U + min(m.u, U - 1)));
+    f.s[r] = pf_b64(st.ue_state + (ec * U + min(m.u, U - 1)));
   }
-  const int ej = min(e0 + (lane < RG ? lane : min(lane - RG, RG - 1)), elast);
-  f.td = at(lane < RG ? st.t : tb.drawn, 4u * (uint32_t)ej);
-  const int ep = min(e0 + min(lane >> 1, RG - 1), elast);
-  f.pc = at(reinterpret_cast<v4u32*>(st.pcg), 48u * (uint32_t)ep + 16u * (uint32_t)(lane & 1));
+  const int ej = min(e0 + min(lane, RG - 1), elast);
+  f.t = pf_b32(st.t + ej);
+  f.d = pf_b32(tb.drawn + ej);
+  if (PE) f.c = pf_b32((st.bs_count ? st.bs_count : st.t) + ej);  // (no count array: B, below)
+  const int ep = min(e0 + min(lane >> 2, RG - 1), elast);
+  f.pc = pf_b64(reinterpret_cast<const char*>(st.pcg) + 48u * (uint32_t)ep + 8u * (uint32_t)(lane & 3));
   const int lim = max(1, min(RG * M, (kp.E - e0) * M));
   const int* src = tb.tab_xy + (size_t)e0 * M;
 #pragma unroll
-  for (int q = 0; q < NT; ++q) f.tab[q] = src[min(q * 64 + lane, lim - 1)];
+  for (int q = 0; q < NT; ++q) f.tab[q] = pf_b32(src + min(q * 64 + lane, lim - 1));
+  if (PE) {
+#pragma unroll
+    for (int q = 0; q < NK; ++q) {
+      const int i = q * 64 + lane;
+      const int es = min(e0 + (i >> 4), elast), k = min(i & 15, KPS(B) - 1);
+      f.bq[q] = pf_b64(st.bs_xy + ((size_t)es * KPS(B) + k));
+    }
+  }
 }
 
 // The prefetched inputs into the pair's contexts and the wave's LDS (draw tables, stream
-// slots; t / drawn through `scratch`, a free histogram area).
-template <int UC, int SCN, int R, int NT>
-__device__ __forceinline__ void lds2_consume(const KParams& kp, const LaneMap& m, int lane, int p,
-                                             const Pre2<R, NT>& f, Ctx2 (&c)[R],
-                                             int* __restrict__ ltab, u128* __restrict__ lpcg,
-                                             int* __restrict__ scratch) {
+// slots, per-env station keys; t / drawn / counts through `scratch`, a free histogram area).
+template <int UC, int SCN, int R, bool PE, int NT, int NK>
+__device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st, const LaneMap& m,
+                                             int lane, int p, Pre2<R, NT, NK>& f, bool saturated,
+                                             Ctx2 (&c)[R], int* __restrict__ ltab,
+                                             u128* __restrict__ lpcg, int* __restrict__ scratch,
+                                             int* __restrict__ lkeys) {
   constexpr int PC = pitch_of(UC), G = 64 / PC, RG = R * G;
   const int M = KPS(tab_m);
+  lds2_pf_wait<R, NT, NK, PE>(f, saturated);
   const int lim = max(1, min(RG * M, (kp.E - p * RG) * M));
 #pragma unroll
   for (int q = 0; q < NT; ++q)
     if (q * 64 + lane < lim) ltab[q * 64 + lane] = f.tab[q];
-  if (lane < 2 * RG) {
-    reinterpret_cast<v4u32*>(lpcg)[lane] = f.pc;
-    scratch[lane] = f.td;
+  if (lane < 4 * RG) reinterpret_cast<v2u32*>(lpcg)[lane] = f.pc;
+  if (lane < RG) {
+    scratch[lane] = f.t;
+    scratch[RG + lane] = f.d;
+    // (the station count: 0 for slots past the batch's last env)
+    if (PE) scratch[2 * RG + lane] = p * RG + lane < kp.E ? (st.bs_count ? f.c : KPS(B)) : 0;
   }
   __builtin_amdgcn_wave_barrier();
+  if (PE) {
+    // the env's station keys, 16 slots per env, {m = -16 q (int16x2), c = ((|q|^2 + 2^21) << 4)
+    // | k}: the key of station k for a UE at p is dot2(2 p, m) + c (see k_steps_packed); slots
+    // past the env's count hold {0, UINT_MAX}, a key that never wins
+#pragma unroll
+    for (int q = 0; q < NK; ++q) {
+      const int i = q * 64 + lane, slot = i >> 4, k = i & 15;
+      int2 kv = make_int2(0, -1);
+      if (k < scratch[2 * RG + slot]) {
+        const int2 bq = make_int2((int)f.bq[q].x, (int)f.bq[q].y);
+        const s16x2 m2 = {(short)(-16 * bq.x), (short)(-16 * bq.y)};
+        kv = make_int2(__builtin_bit_cast(int, m2),
+                       (int)(((unsigned)(bq.x * bq.x + bq.y * bq.y + (1 << 21)) << 4) | (unsigned)k));
+      }
+      *reinterpret_cast<int2*>(lkeys + slot * 32 + 2 * k) = kv;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int slot = r * G + m.seg;
@@ -1833,10 +1936,11 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const LaneMap& m
     // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
     c[r].s_ok = c[r].drawn > M;
     c[r].moved = false;
-    const int2 v = f.s[r];
+    const int2 v = make_int2((int)f.s[r].x, (int)f.s[r].y);
     c[r].pos = make_int2((int)(short)v.x, v.x >> 16);
     c[r].wp = make_int2((int)(short)v.y, v.y >> 16);
   }
+  __builtin_amdgcn_wave_barrier();
 }
 
 // LDS of k_steps_lds2 per wave: stream slots [R G][2] u128, (PE) station keys [R G][16][2] int,
@@ -1879,89 +1983,109 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const float lower = (float)kp.lower;
   const int pb0 = block_slot(kp.xcd_remap) * NW;
   constexpr int NT = lds2_pre_words<UC, SCN, R>();
-  Pre2<R, NT> f;  // the inputs of the wave's next pair
-  {  // the tables (LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...) and the first pair's
-     // inputs, issued together before one wait
+  constexpr int NK = PE ? (R * G * 16 + 63) / 64 : 1;
+  Pre2<R, NT, NK> f;  // the inputs of the wave's next pair
+  Ctx2 c[R];
+  MEV_TS(0);
+  {  // the tables: LDS-DMA, wave w moves 1 KB pieces w, w + NW, ... (waited for below, with the
+     // first pair's inputs)
     const int n16 = KPS(lds_assoc) >> 4;
     for (int q = wv; q * 64 < n16; q += NW)
       if (q * 64 + lane < n16) glds(tb.lds_blob + q * 64 + lane, reinterpret_cast<int4*>(lds_all) + q * 64);
-    if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, NT>(kp, st, tb, m, lane, pb0 + wvu, f);
-    wait_vmem();
-    __syncthreads();
   }
-  // staged per-env rows: a pair whose steps fit twice in the window alternates between its two
-  // halves (one barrier per flush), else the window cycles (two)
+  // Software pipeline over the workgroup's pair tiles: iteration k issues the loads of tile k's
+  // pair, runs tile k - 1's pair (steps, state stores), then moves tile k's inputs into the
+  // contexts / LDS (lds2_consume) and flushes tile k - 1's staged rows. One prefetch site and
+  // one wait site: the prefetched registers are never carried around a loop edge (a copy there
+  // would read them before the loads land, tools/check_prefetch_regs.py). Every store between
+  // a prefetch and its wait is unconditional -- the trajectory rows of every step, the state's
+  // buffer stores below -- so that 4 nsteps + 8 >= 64 of them make the wait free (vmcnt(63)).
+  // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
+  // halves (one barrier per flush), else the window cycles (two).
   const bool alt = 2 * nsteps <= stage_rows;
+  const bool saturated = 4 * nsteps + 8 >= 64;
   int hb = 0;  // the pair's first row slot (alt)
-  for (int pb = pb0; pb < npairs; pb += gstride, hb = alt ? nsteps - hb : 0) {
-    const int p = pb + wvu;
-    const int e0 = pb * G * R;  // the workgroup tile's first env
+  const bool leader = m.u == PC - 1;
+  const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
+  const uint32_t bst = 8u * (uint32_t)(kp.E * U), bt = 4u * (uint32_t)kp.E;
+  int it = 0;  // (MEV_TIMING)
+  (void)it;
+  for (int pb = pb0 - gstride; pb < npairs; pb += gstride) {
+    const bool first = pb < pb0;              // (uniform: no current tile yet)
+    const int p = pb + wvu, pn = p + gstride;  // this wave's current / next pair
+    const bool cur_ok = !first && p < npairs, nxt_ok = pn < npairs;
+    if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK>(kp, st, tb, m, lane, pn, f);
+    if (first) {  // the tables and the first pair's inputs landed
+      wait_vmem();
+      __syncthreads();
+      MEV_TS(1);
+    }
     int* const sw = srow + hb * NWG;
     uint8_t* const dw = drow + hb * NWG;
-    if (p >= npairs) {  // no pair for this wave: its part of the flushes only
-      for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-        flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
-                      NWG, !alt);
-      continue;
-    }
-    Ctx2 c[R];
-    int e[R], nok[R];
-    bool env_ok[R];
-    const bool leader = m.u == PC - 1;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int g = 2 * p + r;
-      e[r] = g * G + m.seg;
-      env_ok[r] = (m.seg < G) && (e[r] < kp.E);
-      nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
-    }
-    if (PE) {  // the envs' station keys (see k_steps_packed's staging), before the next pair's
-               // loads are issued (their wait then leaves those in flight)
+    const int e0 = pb * G * R;  // the current tile's first env
+    if (cur_ok) {
+      int e[R], nok[R];
+      bool env_ok[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int ec = min(e[r], kp.E - 1);
-        const int nbf = env_ok[r] ? (st.bs_count ? st.bs_count[ec] : B) : 0;
-        for (int k = m.u; k < 16; k += PC) {
-          int2 kv = make_int2(0, -1);
-          if (k < nbf) {
-            const int2 q = st.bs_xy[(size_t)ec * B + k];
-            const s16x2 m2 = {(short)(-16 * q.x), (short)(-16 * q.y)};
-            kv = make_int2(__builtin_bit_cast(int, m2),
-                           (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << 4) | (unsigned)k));
-          }
-          *reinterpret_cast<int2*>(lkeys + (r * G + m.seg) * 32 + 2 * k) = kv;
-        }
+        const int g = 2 * p + r;
+        e[r] = g * G + m.seg;
+        env_ok[r] = (m.seg < G) && (e[r] < kp.E);
+        nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
       }
-    }
-    lds2_consume<UC, SCN, R, NT>(kp, m, lane, p, f, c, ltab, lpcg, hist);
-    if (p + gstride < npairs) lds2_prefetch<UC, SCN, R, NT>(kp, st, tb, m, lane, p + gstride, f);
-    const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
-    for (int i = 0, sr = 0; i < nsteps; ++i, sr = sr + 1 == stage_rows ? 0 : sr + 1) {
-      lds2_step<UC, SCN, R, PE, TF>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
-                                lblob, lpcg, hist, ltab, sw + sr * NWG + wvu * G * R,
-                                dw + sr * NWG + wvu * G * R, lkeys);
-      if (sr + 1 == stage_rows || i + 1 == nsteps)
-        flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, !alt);
-    }
-    // the state after the last step (see k_steps_packed); the stream state only where the slot
-    // holds it (draws past the table, mev_state.pcg): no global load here, whose wait would
-    // drain every store of the pair
+      int i = 0, sr = 0;
+      do {  // (nsteps >= 1: the loop body runs at least once)
+        lds2_step<UC, SCN, R, PE, TF>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
+                                      lblob, lpcg, hist, ltab, sw + sr * NWG + wvu * G * R,
+                                      dw + sr * NWG + wvu * G * R, lkeys);
+        if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
+          flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+        ++i;
+        sr = sr + 1 == stage_rows ? 0 : sr + 1;
+      } while (i < nsteps);
+      MEV_TS(min(3 + 3 * it, 27));
+      // the state after the last step (see k_steps_packed), as unconditional buffer stores; the
+      // stream state only where the slot holds it (draws past the table, mev_state.pcg): no
+      // global load here, whose wait would drain every store of the pair
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (env_ok[r] && m.u < U)
-        store_ue(&at(st.ue_state, 8u * (uint32_t)(e[r] * U + m.u)), c[r].pos, c[r].wp);
-      const bool mvd = seg_field<PC>(bal(c[r].moved), m) != 0u;
-      if (env_ok[r] && leader) {
-        at(st.t, 4u * (uint32_t)e[r]) = c[r].t;
-        at(tb.drawn, 4u * (uint32_t)e[r]) = c[r].drawn;
-        if (mvd && c[r].s_ok) {
-          const u128 sl = lpcg[2 * (r * G + m.seg)];
-          at(reinterpret_cast<ulonglong2*>(st.pcg), 48u * (uint32_t)e[r]) =
-              make_ulonglong2((uint64_t)sl, (uint64_t)(sl >> 64));
-        }
+      for (int r = 0; r < R; ++r) {
+        const int2 pw = make_int2((int)(((unsigned)c[r].pos.x & 0xffffu) | ((unsigned)c[r].pos.y << 16)),
+                                  (int)(((unsigned)c[r].wp.x & 0xffffu) | ((unsigned)c[r].wp.y << 16)));
+        const v2u32 pv = {(unsigned)pw.x, (unsigned)pw.y};
+        __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
+                                              env_ok[r] && m.u < U ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
+        const bool mvd = seg_field<PC>(bal(c[r].moved), m) != 0u;
+        const bool ld = env_ok[r] && leader;
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].t, out_rsrc(st.t, bt),
+                                              ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].drawn, out_rsrc(tb.drawn, bt),
+                                              ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
+        const u128 sl = lpcg[2 * (r * G + m.seg)];
+        const v4u32 sv = {(unsigned)(uint64_t)sl, (unsigned)((uint64_t)sl >> 32),
+                          (unsigned)(uint64_t)(sl >> 64), (unsigned)((uint64_t)(sl >> 64) >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(sv, out_rsrc(st.pcg, 12u * bt),
+                                               ld && mvd && c[r].s_ok ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
       }
+    }
+    if (nxt_ok) {  // the next pair's inputs (waited for: free after a whole pair's stores)
+      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pn, f, cur_ok && saturated, c, ltab,
+                                           lpcg, hist, lkeys);
+      MEV_TS(first ? 2 : min(4 + 3 * it, 28));
+    }
+    if (!first) {
+      if (alt) {
+        flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
+      } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
+        for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
+          flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
+                        NWG, true);
+      }
+      MEV_TS(min(5 + 3 * it, 29));
+      hb = alt ? nsteps - hb : 0;
+      ++it;
     }
   }
+  MEV_TS(31);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3878,6 +4002,13 @@ int mev_prepare_draws(const mev_ctx* c, const mev_state* st, const uint8_t* env_
   MEV_HIP(hipGetLastError());
   return MEV_OK;
 }
+
+#ifdef MEV_TIMING
+extern "C" int mev_debug_timestamps(void* dev_buf) {
+  MEV_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mev_ts), &dev_buf, sizeof(void*)));
+  return MEV_OK;
+}
+#endif
 
 int mev_sync_stream_state(const mev_ctx* c, const mev_state* st, void* stream) {
   if (!c || !st || !st->pcg) return MEV_EINVAL;

@@ -288,6 +288,30 @@ def test_store_hazard_check_on_generated_assembly():
     assert ch.violations(text) == []
 
 
+def test_prefetch_registers_check_on_generated_assembly():
+    """The two-group rollout kernel's one-pair-ahead input loads are inline assembly the
+    compiler does not track (mev_step.hip, pf_b32 / pf_b64); the kernel waits for them itself.
+    tools/check_prefetch_regs.py verifies on `make asm` output that every prefetched value stays
+    in the register its load wrote, untouched, until the explicit wait -- no copy, no spill,
+    no reuse -- in every kernel instance that has them; and the checker flags a copy."""
+    import shutil
+    import sys
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        pytest.skip("hipcc not available")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_prefetch_regs as cp
+    bad = ("_Zk:\n\tglobal_load_dword v5, v[2:3], off ; mev-prefetch\n"
+           "\tv_mov_b32_e32 v9, v5\n\t; mev-prefetch-wait v9\n")
+    assert cp.violations(bad)[0]
+    good = ("_Zk:\n\tglobal_load_dword v5, v[2:3], off ; mev-prefetch\n"
+            "\tv_add_u32_e32 v7, v8, v6\n\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v5\n"
+            "\tds_write_b32 v1, v5\n")
+    assert cp.violations(good) == ([], 1)
+    text = open(cp.build_asm()).read()
+    v, n = cp.violations(text)
+    assert n >= 8 and v == []
+
+
 def test_host_code_under_asan(tmp_path, golden_dir):
     """The library's host code (argument checks, numpy-compatible seeding, the libm channel
     table, mev_create's validation and failure path) under AddressSanitizer + UBSan with leak

@@ -137,3 +137,37 @@ def test_bench_multi_rank_glue(tmp_path):
     np.testing.assert_array_equal(g[:, 0].numpy(), want.astype(np.float32))
     np.testing.assert_array_equal(g[:, 1].numpy(), np.zeros((world, 5), np.float32))
     assert r["value"] == world * 5 * 23 / r["elapsed"]
+
+
+def test_bench_spawns_its_own_ranks():
+    """`python bench.py --gpus 2` as a plain command (no launcher, WORLD_SIZE unset) starts its
+    two ranks itself; with the CPU stand-in engine (gloo) the line reports n_gpus 2, the world
+    size the ranks saw, exactly K steps, and a final (reward, done) batch / obs gather holding
+    every rank's envs: after W + K steps env g's reward is its seed 1000 + g plus the steps."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    E, K, W = 5, 23, 4
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--stub-engine", "--steps", str(K), "--warmup", str(W), "--chunk", "10",
+                        "--envs", str(E), "--warmup-floor-s", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == K and out["config"]["global_envs"] == 2 * E
+    dd = out["distributed"]
+    assert dd["world_size_seen"] == 2 and dd["backend"] == "gloo"
+    steps = W + K
+    seeds = 1000 + np.arange(2 * E)
+    assert dd["final_batch"]["shape"] == [2, 2, E]
+    assert dd["final_batch"]["reward_sum"] == float((seeds + steps).sum())
+    assert dd["final_batch"]["done_sum"] == float(2 * E * (steps % 20 == 0))
+    og = dd["obs_gather"]
+    U = 30  # mobile-large-central-v0
+    assert og["shape"] == [2, E, U, 4] and og["bytes_per_rank"] == E * U * 16
+    assert og["checksum"] == float(seeds.sum() * U)
+    assert out["value"] == pytest.approx(2 * E * K / (out["ms_per_step"] * K * 1e-3))

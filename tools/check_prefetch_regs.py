@@ -1,0 +1,127 @@
+"""Static check of k_steps_lds2's inline-assembly prefetch loads in libmev's device assembly.
+
+The one-pair-ahead input loads of the two-group rollout kernel are inline assembly
+(mev_step.hip, pf_b32 / pf_b64: "; mev-prefetch"), which the compiler does not track: the
+hardware writes their destination registers whenever the loads land, and the kernel waits for
+them itself (lds2_pf_wait: an explicit s_waitcnt, then every register tied to it by an empty
+asm, "; mev-prefetch-wait"). That is only sound if the compiler keeps each prefetched value in
+the register the load wrote until that wait: no copy (a copy would read the register before the
+data landed) and no spill. This check, per kernel with prefetch loads:
+  * the registers tied at the waits are exactly the registers the loads wrote (a split live
+    range -- a copy at a loop edge -- shows as a tied register that no load wrote);
+  * no instruction between a prefetch load and the next wait in the code reads one of the
+    loaded registers (copies, spills, any use), other than further prefetch loads;
+  * no instruction between them writes one (a register reused while the load is in flight).
+
+python tools/check_prefetch_regs.py [file.s]   (default: builds `make asm` and checks it)
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mobile-env-gan_amd", "csrc")
+ASM = os.path.join(ROOT, "mobile-env-gan_amd", "lib", "mev_step-gfx950.s")
+
+_REG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+_KERNEL = re.compile(r"^(_Z\S+):")
+
+
+def regs_of(text: str):
+    out = set()
+    for m in _REG.finditer(text):
+        if m.group(1) is not None:
+            out.add(int(m.group(1)))
+        else:
+            out.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def _split_operands(line: str):
+    code = line.split(";")[0].strip()
+    parts = code.split(None, 1)
+    if len(parts) < 2:
+        return parts[0] if parts else "", []
+    return parts[0], [o.strip() for o in parts[1].split(",")]
+
+
+def check_kernel(name: str, lines):
+    """Violations [(line, text, reason)] in one kernel's lines [(number, text)]."""
+    bad = []
+    loaded, tied = set(), set()
+    inflight = set()  # registers of loads issued since the last wait
+    for no, text in lines:
+        if "; mev-prefetch-wait" in text:
+            regs = regs_of(text.split("mev-prefetch-wait", 1)[1])
+            tied |= regs
+            inflight -= regs
+            continue
+        if "; mev-prefetch" in text:
+            op, ops = _split_operands(text)
+            dst = regs_of(ops[0]) if ops else set()
+            loaded |= dst
+            inflight |= dst
+            continue
+        if not inflight:
+            continue
+        code = text.split(";")[0]
+        if not code.strip() or code.strip().startswith(".") or code.strip().endswith(":"):
+            continue
+        op, ops = _split_operands(text)
+        if not ops:
+            continue
+        # operands: the first is the destination for VALU / loads / moves; stores read all
+        used = regs_of(",".join(ops))
+        hit = used & inflight
+        if hit:
+            bad.append((no, text.strip(), f"touches in-flight prefetch register(s) v{sorted(hit)}"))
+    if loaded != tied:
+        bad.append((lines[0][0], name,
+                    f"registers loaded {sorted(loaded - tied)} not tied at a wait / tied "
+                    f"{sorted(tied - loaded)} not loaded"))
+    return bad, len(loaded)
+
+
+def violations(asm_text: str):
+    """(violations, number of kernels with prefetch loads)."""
+    kernels = []
+    cur = None
+    for no, line in enumerate(asm_text.split("\n"), 1):
+        m = _KERNEL.match(line)
+        if m:
+            cur = (m.group(1), [])
+            kernels.append(cur)
+            continue
+        if cur is not None:
+            cur[1].append((no, line))
+            if line.startswith("\t.end_amdhsa_kernel") or line.startswith(".Lfunc_end"):
+                cur = None
+    bad, n = [], 0
+    for name, lines in kernels:
+        if not any("; mev-prefetch" in t for _, t in lines):
+            continue
+        n += 1
+        b, _ = check_kernel(name, lines)
+        bad += [(no, txt, why, name) for no, txt, why in b]
+    return bad, n
+
+
+def build_asm() -> str:
+    subprocess.run(["make", "-C", CSRC, "asm"], check=True, stdout=subprocess.DEVNULL)
+    return ASM
+
+
+def main():
+    path = sys.argv[1] if len(sys.argv) > 1 else build_asm()
+    bad, n = violations(open(path).read())
+    for no, txt, why, name in bad:
+        print(f"{path}:{no}: {why}: {txt} ({name[:60]})")
+    print(f"{n} kernels with prefetch loads, {len(bad)} violations")
+    return 1 if bad or n == 0 else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
