@@ -1,7 +1,7 @@
 #!/bin/bash
 # Dev tool: build libmev_<name>.so from mev_step.hip at git revision <rev> ("WT" = working tree)
 # with the Makefile's flags (plus $EXTRA, e.g. -DMEV_LDS2_WAVES=8), for interleaved timing with tools/gpu_variants.sh
-# or bench lines "MEV_LIB=mobile-env-gan_amd/lib/libmev_<name>.so::ARGS" of tools/gpu_dev.sh.
+# or any tool run with MEV_LIB=$PWD/mobile-env-gan_amd/lib/libmev_<name>.so (tools/launch_len.py, tools/ts_probe.py).
 set -e
 rev=$1; name=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
