@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 14
+#define MEV_ABI_VERSION 15
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -264,6 +264,13 @@ int mev_step(const mev_ctx* ctx, const mev_state* st, const mev_outputs* out,
  * (per-episode, accumulated as in mev_step). Same results as nsteps mev_step calls. */
 int mev_rollout(const mev_ctx* ctx, const mev_state* st, const mev_outputs* traj,
                 int32_t nsteps, void* stream);
+
+/* mev_rollout with timing events (hipEvent_t, created by the caller; either may be NULL): a
+ * launch of one kernel records them from its own dispatch (hipExtLaunchKernelGGL: the kernel's
+ * start and end; no marker packets and no system-scope fence of separate event records around
+ * it); launches of several kernels record them before the first and after the last. */
+int mev_rollout_timed(const mev_ctx* ctx, const mev_state* st, const mev_outputs* traj,
+                      int32_t nsteps, void* stream, void* start_event, void* stop_event);
 
 /* Error text for a return code; last HIP error string for MEV_EHIP. */
 const char* mev_strerror(int code);

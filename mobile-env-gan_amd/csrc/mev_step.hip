@@ -27,6 +27,7 @@
 // HIP's float64 '/', sqrt and rint are IEEE correctly rounded, so positions, serving
 // indices and the rounded rates match the reference exactly (tests/ check it).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <climits>
 #include <cmath>
@@ -1987,19 +1988,28 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   Pre2<R, NT, NK> f;  // the inputs of the wave's next pair
   Ctx2 c[R];
   MEV_TS(0);
-  {  // the tables: LDS-DMA, wave w moves 1 KB pieces w, w + NW, ... (waited for below, with the
-     // first pair's inputs)
+  {  // the tables (LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...) and the first pair's
+     // inputs, issued together before one wait (before the pair loop: a wait inside it would
+     // leave the compiler unsure the copy is done, and it would wait before LDS accesses)
     const int n16 = KPS(lds_assoc) >> 4;
     for (int q = wv; q * 64 < n16; q += NW)
       if (q * 64 + lane < n16) glds(tb.lds_blob + q * 64 + lane, reinterpret_cast<int4*>(lds_all) + q * 64);
+    if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, PE, NT, NK>(kp, st, tb, m, lane, pb0 + wvu, f);
+    wait_vmem();
+    __syncthreads();
+    MEV_TS(1);
+    if (pb0 + wvu < npairs)
+      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pb0 + wvu, f, false, c, ltab, lpcg,
+                                           hist, lkeys);
+    MEV_TS(2);
   }
-  // Software pipeline over the workgroup's pair tiles: iteration k issues the loads of tile k's
-  // pair, runs tile k - 1's pair (steps, state stores), then moves tile k's inputs into the
-  // contexts / LDS (lds2_consume) and flushes tile k - 1's staged rows. One prefetch site and
-  // one wait site: the prefetched registers are never carried around a loop edge (a copy there
-  // would read them before the loads land, tools/check_prefetch_regs.py). Every store between
-  // a prefetch and its wait is unconditional -- the trajectory rows of every step, the state's
-  // buffer stores below -- so that 4 nsteps + 8 >= 64 of them make the wait free (vmcnt(63)).
+  // Software pipeline over the workgroup's pair tiles: iteration k issues the loads of the wave's
+  // pair of tile k + 1, runs its pair of tile k (steps, state stores), then moves the next
+  // pair's inputs into the contexts / LDS (lds2_consume) and flushes tile k's staged rows. The
+  // prefetched registers are never carried around a loop edge (a copy there would read them
+  // before the loads land, tools/check_prefetch_regs.py). Every store between a prefetch and
+  // its wait is unconditional -- the trajectory rows of every step, the state's buffer stores
+  // below -- so that 4 nsteps + 8 >= 64 of them make the wait free (vmcnt(63)).
   // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
   // halves (one barrier per flush), else the window cycles (two).
   const bool alt = 2 * nsteps <= stage_rows;
@@ -2010,16 +2020,10 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const uint32_t bst = 8u * (uint32_t)(kp.E * U), bt = 4u * (uint32_t)kp.E;
   int it = 0;  // (MEV_TIMING)
   (void)it;
-  for (int pb = pb0 - gstride; pb < npairs; pb += gstride) {
-    const bool first = pb < pb0;              // (uniform: no current tile yet)
+  for (int pb = pb0; pb < npairs; pb += gstride) {
     const int p = pb + wvu, pn = p + gstride;  // this wave's current / next pair
-    const bool cur_ok = !first && p < npairs, nxt_ok = pn < npairs;
+    const bool cur_ok = p < npairs, nxt_ok = pn < npairs;
     if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK>(kp, st, tb, m, lane, pn, f);
-    if (first) {  // the tables and the first pair's inputs landed
-      wait_vmem();
-      __syncthreads();
-      MEV_TS(1);
-    }
     int* const sw = srow + hb * NWG;
     uint8_t* const dw = drow + hb * NWG;
     const int e0 = pb * G * R;  // the current tile's first env
@@ -2068,22 +2072,20 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       }
     }
     if (nxt_ok) {  // the next pair's inputs (waited for: free after a whole pair's stores)
-      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pn, f, cur_ok && saturated, c, ltab,
-                                           lpcg, hist, lkeys);
-      MEV_TS(first ? 2 : min(4 + 3 * it, 28));
+      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pn, f, saturated, c, ltab, lpcg, hist,
+                                           lkeys);
+      MEV_TS(min(4 + 3 * it, 28));
     }
-    if (!first) {
-      if (alt) {
-        flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
-      } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
-        for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-          flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
-                        NWG, true);
-      }
-      MEV_TS(min(5 + 3 * it, 29));
-      hb = alt ? nsteps - hb : 0;
-      ++it;
+    if (alt) {
+      flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
+    } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
+      for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
+        flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
+                      NWG, true);
     }
+    MEV_TS(min(5 + 3 * it, 29));
+    hb = alt ? nsteps - hb : 0;
+    ++it;
   }
   MEV_TS(31);
 }
@@ -3794,11 +3796,33 @@ static StepsKernel steps_kernel_for(bool per_env, bool lean, int ldsm, int U) {
   return lean ? steps_kernel_u<false, true, 0>(U) : steps_kernel_u<false, false, 0>(U);
 }
 
+// Timing events of a launch (mev_rollout_timed): a single-kernel launch has its dispatch record
+// them (hipExtLaunchKernelGGL: the kernel's own start and end, no separate marker packets and
+// no system-scope fence of an event record); launches of several kernels record them around.
+struct LaunchEv {
+  hipEvent_t start, stop;
+  bool on() const { return start != nullptr || stop != nullptr; }
+};
+
+template <class K, class... A>
+static void launch_k(K kern, dim3 grid, dim3 block, size_t shmem, hipStream_t stream,
+                     const LaunchEv& ev, A... args) {
+  if (ev.on())
+    hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)shmem, stream, ev.start, ev.stop, 0u, args...);
+  else
+    hipLaunchKernelGGL(kern, grid, block, shmem, stream, args...);
+}
+
+static int launch_packed_split(const mev_ctx* c, const KState& ks, const KOut& ko,
+                               const KTables& tb, int nsteps, bool traj, hipStream_t stream,
+                               StepKernel k, size_t shmem, int groups);
+
 // Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
 // the caller's stream, the second on c->aux (forked from and joined back into the caller's
 // stream); the halves are independent envs, so the two streams overlap freely.
 static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& ko,
-                               const KTables& tb, int nsteps, bool traj, hipStream_t stream) {
+                               const KTables& tb, int nsteps, bool traj, hipStream_t stream,
+                               const LaunchEv& ev) {
   const KParams& kp = c->kp;
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
@@ -3833,8 +3857,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       const size_t sh = (size_t)kp.lds_assoc +
                         kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2, true) +
                         (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
-      k2<<<dim3(blocks), dim3(64 * kLds2Waves), sh, stream>>>(kp, ks, ko, tb, groups, nsteps, 1,
-                                                              srows);
+      launch_k(k2, dim3(blocks), dim3(64 * kLds2Waves), sh, stream, ev, kp, ks, ko, tb, groups,
+               nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
       return MEV_OK;
     }
@@ -3852,8 +3876,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       const int srows = std::min(c->stage_rows2, nsteps);
       const size_t sh = (size_t)kp.lds_assoc + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2) +
                         (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
-      k2<<<dim3(blocks), dim3(64 * kLds2Waves), sh, stream>>>(kp, ks, ko, tb, groups, nsteps, 1,
-                                                              srows);
+      launch_k(k2, dim3(blocks), dim3(64 * kLds2Waves), sh, stream, ev, kp, ks, ko, tb, groups,
+               nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
       return MEV_OK;
     }
@@ -3876,11 +3900,23 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       srows = std::min({nsteps, c->stage_cap > 0 ? c->stage_cap : nsteps,
                         (int)(((size_t)kLds2BytesPerWG - shmem_f - 4) /
                               ((size_t)nw * stage_bytes_per_row(kp)))});
-    kf<<<dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
-         stream>>>(kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
+    launch_k(kf, dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
+             stream, ev, kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
     MEV_HIP(hipGetLastError());
     return MEV_OK;
   }
+  // (several kernels: the timing events around them)
+  if (ev.start) MEV_HIP(hipEventRecord(ev.start, stream));
+  const int rc = launch_packed_split(c, ks, ko, tb, nsteps, traj, stream, k, shmem, groups);
+  if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, stream));
+  return rc;
+}
+
+// One-step kernels, nsteps launches, one stream or two env halves (mev_step's shapes)
+static int launch_packed_split(const mev_ctx* c, const KState& ks, const KOut& ko,
+                               const KTables& tb, int nsteps, bool traj, hipStream_t stream,
+                               StepKernel k, size_t shmem, int groups) {
+  const KParams& kp = c->kp;
   // split on a block boundary
   const int half = (groups / 2 + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
   if (c->parts == 1 || half <= 0 || half >= groups) {
@@ -3909,7 +3945,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
 // Block-shape steps (U > 64): ONE launch of k_steps_block for the n steps (fuse_steps), or one
 // per step; one workgroup per env.
 static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko,
-                              const KTables& tb, int nsteps, bool traj, hipStream_t stream) {
+                              const KTables& tb, int nsteps, bool traj, hipStream_t stream,
+                              const LaunchEv& ev) {
   const KParams& kp = c->kp;
   if (nsteps <= 0) return MEV_OK;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
@@ -3924,11 +3961,13 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
     kf = c->tie_free ? k_steps_block<true, true, false, 4, true> : k_steps_block<true, true, false, 4>;
   const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
   if (c->fuse_steps || nsteps == 1) {
-    kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, ko, tb, nsteps, traj ? 1 : 0);
+    launch_k(kf, dim3(kp.E), block, shm, stream, ev, kp, ks, ko, tb, nsteps, traj ? 1 : 0);
   } else {
+    if (ev.start) MEV_HIP(hipEventRecord(ev.start, stream));
     for (int i = 0; i < nsteps; ++i)
       kf<<<dim3(kp.E), block, shm, stream>>>(kp, ks, traj ? out_row(ko, kp.E, kp.U, i) : ko, tb,
                                              1, 0);
+    if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, stream));
   }
   MEV_HIP(hipGetLastError());
   return MEV_OK;
@@ -3949,13 +3988,13 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
       hipLaunchKernelGGL(k_reset_packed, grid, dim3(kPackedBlock), 0, stream, kp, ks, ko, tb,
                          mask);
     } else {
-      return launch_packed_steps(c, ks, ko, tb, 1, false, stream);
+      return launch_packed_steps(c, ks, ko, tb, 1, false, stream, LaunchEv{nullptr, nullptr});
     }
   } else if (RESET) {
     const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
     hipLaunchKernelGGL(k_reset_block, dim3(kp.E), block, 0, stream, kp, ks, ko, tb, mask);
   } else {
-    return launch_block_steps(c, ks, ko, tb, 1, false, stream);
+    return launch_block_steps(c, ks, ko, tb, 1, false, stream, LaunchEv{nullptr, nullptr});
   }
   MEV_HIP(hipGetLastError());
   return MEV_OK;
@@ -4031,7 +4070,7 @@ int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
 }
 
 static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
-                     int32_t nsteps, bool traj, void* stream) {
+                     int32_t nsteps, bool traj, void* stream, LaunchEv ev = LaunchEv{nullptr, nullptr}) {
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   if (nsteps < 0) return MEV_EINVAL;
@@ -4039,9 +4078,14 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
   KOut ko;
   to_kernel(st, out, ks, ko);
   const KTables tb = tables_of(c);
+  if (nsteps == 0 && ev.on()) {  // nothing to launch: the events still bracket the (empty) work
+    if (ev.start) MEV_HIP(hipEventRecord(ev.start, (hipStream_t)stream));
+    if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, (hipStream_t)stream));
+    return MEV_OK;
+  }
   if (c->kp.U <= 64 && !c->kp.het)
-    return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
-  return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream);
+    return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
+  return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
 }
 
 int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int32_t nsteps,
@@ -4052,6 +4096,12 @@ int mev_step(const mev_ctx* c, const mev_state* st, const mev_outputs* out, int3
 int mev_rollout(const mev_ctx* c, const mev_state* st, const mev_outputs* traj,
                 int32_t nsteps, void* stream) {
   return run_steps(c, st, traj, nsteps, true, stream);
+}
+
+int mev_rollout_timed(const mev_ctx* c, const mev_state* st, const mev_outputs* traj,
+                      int32_t nsteps, void* stream, void* start_event, void* stop_event) {
+  return run_steps(c, st, traj, nsteps, true, stream,
+                   LaunchEv{(hipEvent_t)start_event, (hipEvent_t)stop_event});
 }
 
 // --------------------------------------------------------------------------------------

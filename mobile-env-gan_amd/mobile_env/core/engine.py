@@ -202,6 +202,8 @@ class StepEngine:
         device = torch.device(device)
         if device.type != "cuda":
             raise RuntimeError("StepEngine runs on a ROCm GPU only (no CPU fallback)")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         self.device = device
         self.p = params
         E, U = params.num_envs, params.num_ues
@@ -422,29 +424,52 @@ class StepEngine:
                                           self._stream()), "mev_rollout")
         return traj
 
-    def launcher(self, nsteps: int, traj: "Trajectory | None" = None):
+    def launcher(self, nsteps: int, traj: "Trajectory | None" = None, events=None):
         """A zero-argument callable that issues ``rollout(nsteps, traj)`` (traj given) or
         ``step(nsteps)`` with every ctypes argument prebuilt: the per-call host cost is one
-        foreign call (the benchmark's timed loop; the caller keeps the device current)."""
+        foreign call (the benchmark's timed loop). ``events`` (rollouts only): a (start, stop)
+        pair of HIP event handles the launch records from its own dispatch
+        (mev_rollout_timed). Checks like rollout(): the trajectory must fit and carry the
+        engine's output set; the launch runs on the engine's device."""
         n = int(nsteps)
         st = C.byref(self._st)
-        stream = self._stream()
+        with torch.cuda.device(self.device):
+            stream = self._stream()
         if traj is None:
+            if events is not None:
+                raise ValueError("timing events need a trajectory launch (rollout)")
             fn, out, where = self._lib.mev_step, C.byref(self._out), "mev_step"
         else:
             if traj.obs.shape[0] < n or tuple(traj.obs.shape[1:]) != tuple(self.obs.shape):
                 raise ValueError("trajectory buffers do not fit this engine / nsteps")
+            if (traj.rate64 is None) != (self.rate64 is None) or \
+                    (traj.util64 is None) != (self.util64 is None) or \
+                    (traj.metrics is None) != (self.metrics is None):
+                raise ValueError("trajectory outputs differ from the engine's output set")
             o = N.MevOutputs(_ptr(traj.obs), _ptr(traj.serving), _ptr(traj.reward),
                              _ptr(traj.done), _ptr(traj.rate64), _ptr(traj.util64),
                              _ptr(traj.metrics), _ptr(self.qoe_stats))
             fn, out, where = self._lib.mev_rollout, C.byref(o), "mev_rollout"
         ctx = self._ctx
+        dev = self.device.index
+        if events is not None:
+            fn, where = self._lib.mev_rollout_timed, "mev_rollout_timed"
+            ev0, ev1 = (C.c_void_p(int(e) if e else 0) for e in events)
 
-        def go():
-            rc = fn(ctx, st, out, n, stream)
-            if rc:
-                N.check(rc, where)
-        go.keep = (out, traj)
+            def go():
+                if torch.cuda.current_device() != dev:
+                    raise RuntimeError(f"launcher of cuda:{dev} called with another device current")
+                rc = fn(ctx, st, out, n, stream, ev0, ev1)
+                if rc:
+                    N.check(rc, where)
+        else:
+            def go():
+                if torch.cuda.current_device() != dev:
+                    raise RuntimeError(f"launcher of cuda:{dev} called with another device current")
+                rc = fn(ctx, st, out, n, stream)
+                if rc:
+                    N.check(rc, where)
+        go.keep = (out, traj, events)
         return go
 
     def close(self):

@@ -11,6 +11,9 @@ import statistics
 import sys
 import time
 
+if os.environ.get("SPIN"):  # host wait policy: spin (hipDeviceScheduleSpin), set before any
+    import ctypes as _C       # HIP call creates the device context
+    assert _C.CDLL("libamdhip64.so").hipSetDeviceFlags(_C.c_uint(int(os.environ["SPIN"]))) == 0
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "mobile-env-gan_amd"))
@@ -19,8 +22,31 @@ import mobile_env  # noqa: E402
 E = int(os.environ.get("E", 65536))
 WL = os.environ.get("WL", "mobile-large-central-v0")
 LENS = [int(a) for a in sys.argv[1:]] or [20, 40, 100, 200]
+
+
+class HipEvent:
+    """A HIP event with explicit creation flags (hipEventCreateWithFlags), e.g. timing-only
+    hipEventDisableSystemFence events (no system-scope cache writeback when recorded)."""
+    _hip = None
+
+    def __init__(self, flags):
+        import ctypes as C
+        if HipEvent._hip is None:
+            HipEvent._hip = C.CDLL("libamdhip64.so")
+        self.C = C
+        self.ev = C.c_void_p()
+        assert HipEvent._hip.hipEventCreateWithFlags(C.byref(self.ev), C.c_uint(flags)) == 0
+
+    def record(self, stream):
+        assert HipEvent._hip.hipEventRecord(self.ev, self.C.c_void_p(stream.cuda_stream)) == 0
+
+    def elapsed_time(self, other):
+        ms = self.C.c_float()
+        assert HipEvent._hip.hipEventElapsedTime(self.C.byref(ms), self.ev, other.ev) == 0
+        return ms.value
 over = {k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("MEV_ENGINE", "").split(",")
                                if kv)}
+EVMODE = os.environ.get("EVMODE", "torch")  # torch | nofence (hipEventDisableSystemFence) | none
 env = mobile_env.make(WL, num_envs=E, device="cuda:0", seed=1000, **over)
 env.reset()
 eng = env.engine
@@ -38,16 +64,36 @@ for n in LENS:
         go()
     torch.cuda.synchronize()
     iso_ev, iso_wall = [], []
-    for _ in range(30):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if EVMODE == "inlaunch":  # the launch records its own pair (mev_rollout_timed)
+        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(30)]
+        for a, b in pairs:
+            a.record(stream)
+            b.record(stream)
+        gos = [eng.launcher(n, traj, events=(a.cuda_event, b.cuda_event)) for a, b in pairs]
+        torch.cuda.synchronize()
+        for (a, b), g in zip(pairs, gos):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g()
+            torch.cuda.synchronize()
+            iso_wall.append((time.perf_counter() - t0) * 1e3)
+            iso_ev.append(a.elapsed_time(b))
+    for _ in range(30 if EVMODE != "inlaunch" else 0):
+        if EVMODE == "nofence":
+            a, b = HipEvent(0x20000000), HipEvent(0x20000000)
+        else:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        a.record(stream)
+        if EVMODE != "none":
+            a.record(stream)
         go()
-        b.record(stream)
+        if EVMODE != "none":
+            b.record(stream)
         torch.cuda.synchronize()
         iso_wall.append((time.perf_counter() - t0) * 1e3)
-        iso_ev.append(a.elapsed_time(b))
+        iso_ev.append(a.elapsed_time(b) if EVMODE != "none" else 0.0)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = max(4, 4000 // n)
     a.record(stream)
@@ -56,7 +102,7 @@ for n in LENS:
     b.record(stream)
     torch.cuda.synchronize()
     b2b = a.elapsed_time(b) / reps
-    print(json.dumps({"n": n, "engine": over, "iso_event_ms_median": statistics.median(iso_ev),
+    print(json.dumps({"n": n, "engine": over, "evmode": EVMODE, "spin": os.environ.get("SPIN"), "iso_event_ms_median": statistics.median(iso_ev),
                       "iso_event_ms_min": min(iso_ev),
                       "iso_wall_ms_median": statistics.median(iso_wall),
                       "b2b_ms": b2b, "b2b_us_per_step": b2b * 1e3 / n,
