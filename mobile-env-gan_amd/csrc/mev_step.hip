@@ -1786,9 +1786,28 @@ __device__ uint64_t* g_mev_ts;
     if (g_mev_ts && lane == 0)                                                            \
       g_mev_ts[(size_t)(blockIdx.x * NW + wv) * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define MEV_CLK(k)                                                                        \
+  do {                                                                                    \
+    if (g_mev_ts && lane == 0)                                                            \
+      g_mev_ts[(size_t)(blockIdx.x * NW + wv) * 32 + (k)] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
+// the wave's HW_ID (CU / SIMD / shader engine) and XCC_ID registers
+#define MEV_HWID(k)                                                                       \
+  do {                                                                                    \
+    if (g_mev_ts && lane == 0) {                                                          \
+      g_mev_ts[(size_t)(blockIdx.x * NW + wv) * 32 + (k)] = __builtin_amdgcn_s_getreg(0xF804); \
+      g_mev_ts[(size_t)(blockIdx.x * NW + wv) * 32 + (k) + 1] = __builtin_amdgcn_s_getreg(0xF814); \
+    }                                                                                     \
+  } while (0)
 #else
 #define MEV_TS(k) \
   do {            \
+  } while (0)
+#define MEV_CLK(k) \
+  do {             \
+  } while (0)
+#define MEV_HWID(k) \
+  do {              \
   } while (0)
 #endif
 
@@ -1988,6 +2007,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   Pre2<R, NT, NK> f;  // the inputs of the wave's next pair
   Ctx2 c[R];
   MEV_TS(0);
+  MEV_CLK(25);
+  MEV_HWID(23);
   {  // the tables (LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...) and the first pair's
      // inputs, issued together before one wait (before the pair loop: a wait inside it would
      // leave the compiler unsure the copy is done, and it would wait before LDS accesses)
@@ -2088,6 +2109,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     ++it;
   }
   MEV_TS(31);
+  MEV_CLK(26);
 }
 
 // ------------------------------------------------------------------------------------

@@ -50,7 +50,7 @@ EVMODE = os.environ.get("EVMODE", "torch")  # torch | nofence (hipEventDisableSy
 env = mobile_env.make(WL, num_envs=E, device="cuda:0", seed=1000, **over)
 env.reset()
 eng = env.engine
-traj = eng.trajectory(max(LENS))
+traj = eng.trajectory(int(os.environ.get("TRAJ_ROWS", max(LENS))))  # (buffer size: placement)
 stream = torch.cuda.current_stream()
 t_w = time.perf_counter()
 go = eng.launcher(max(LENS), traj)
@@ -102,7 +102,7 @@ for n in LENS:
     b.record(stream)
     torch.cuda.synchronize()
     b2b = a.elapsed_time(b) / reps
-    print(json.dumps({"n": n, "engine": over, "evmode": EVMODE, "spin": os.environ.get("SPIN"), "iso_event_ms_median": statistics.median(iso_ev),
+    print(json.dumps({"n": n, "engine": over, "evmode": EVMODE, "spin": os.environ.get("SPIN"), "traj_rows": traj.obs.shape[0], "iso_event_ms_median": statistics.median(iso_ev),
                       "iso_event_ms_min": min(iso_ev),
                       "iso_wall_ms_median": statistics.median(iso_wall),
                       "b2b_ms": b2b, "b2b_us_per_step": b2b * 1e3 / n,
