@@ -121,7 +121,7 @@ def max_over_ranks(value: float, device=None) -> float:
 # CPU baseline: the per-object port of the reference step, one process per core
 # ---------------------------------------------------------------------------------------------
 def _cpu_worker(args):
-    layout, num_bs, num_ues, velocity, seed0, budget_s = args
+    layout, num_bs, num_ues, velocity, seed0, budget_s, classes = args
     import numpy as np
     from oracle import port
     done = 0
@@ -131,7 +131,7 @@ def _cpu_worker(args):
         # per-env-layout workloads: a uniform integer layout per episode (vector._bs_layouts)
         lay = layout if layout is not None else \
             np.random.default_rng(seed0 + k).integers(0, 200, size=(num_bs, 2)).tolist()
-        core = port.build(lay, num_ues, seed0 + k, velocity)
+        core = port.build(lay, num_ues, seed0 + k, velocity, classes=classes)
         core.reset()
         for _ in range(20):  # an episode, or as much of it as the budget allows
             core.step()
@@ -166,8 +166,8 @@ def cpu_baseline(budget_s: float, procs: int, workload: str = "mobile-large-cent
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(lay, B, U, vel, 1000 + 100000 * i, budget_s)
-                                     for i in range(procs)])
+        res = pool.map(_cpu_worker, [(lay, B, U, vel, 1000 + 100000 * i, budget_s,
+                                      sp.get("classes")) for i in range(procs)])
     wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",

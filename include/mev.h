@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 15
+#define MEV_ABI_VERSION 16
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -119,7 +119,9 @@ typedef struct mev_params {
    * (at most 16 classes each); a UE connects to the closest station whose pair SNR exceeds its
    * snr_tr (base.py:236-241). rate_table then holds one table per class pair
    * p = cb * num_ue_classes + cu at [rate_table_offsets[p], rate_table_offsets[p + 1]) (NULL
-   * rate_table: built with libm). Heterogeneous contexts run the block kernel for any U. */
+   * rate_table: built with libm). With a shared layout and U <= 64 heterogeneous contexts run the
+   * packed kernels (one association map per UE class, [num_ue_classes][H][W] x 16 B); with
+   * per-env layouts or U > 64, the block kernel. */
   int32_t num_bs_classes, num_ue_classes;
   const int32_t* bs_class;
   const int32_t* ue_class;
@@ -181,6 +183,10 @@ void mev_destroy(mev_ctx* ctx);
 int mev_d2max(const mev_ctx* ctx);
 /* Number of env halves mev_step launches per step (1, or 2 on two streams; stream_split). */
 int mev_launch_parts(const mev_ctx* ctx);
+/* Kernel shape of the context's steps: 1 = packed (one lane per UE, U <= 64: several envs per
+ * wavefront), 2 = block (one workgroup per env: U > 64, or heterogeneous entities with per-env
+ * layouts). */
+int mev_step_shape(const mev_ctx* ctx);
 /* Bytes of the compact association tables rollout launches copy into LDS (shared layouts whose
  * tables fit); 0: rollouts gather from the L2 association map. */
 int mev_lds_tables_bytes(const mev_ctx* ctx);

@@ -777,6 +777,11 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   const int M = KPS(tab_m);  // wave-uniform
   int drawn = cur.drawn;
   bool s_ok = cur.s_ok;
+  // heterogeneous entities (shared layout, L2 association maps only): this UE's class selects
+  // its movement parameters and its class's association map (wave-uniform flag)
+  constexpr bool HETOK = !LDSA && SCN == 0 && !PER_ENV_BS;
+  const bool het = HETOK && kp.het;
+  const int cu = het ? (int)tb.ue_cls[min(u, U - 1)] : 0;
 
   // Stream bookkeeping without cross-lane moves: the step's waypoint draws start at offset
   // koff of stream state `s` (koff = 2U right after a reset: the initial positions took the
@@ -912,7 +917,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
       else if (tot > 0 || reset_env) s_ok = false;
     }
   }
-  if (active) move_ue<SCN>(pos, wp, kp);
+  if (active) {
+    if (het) move_ue_p(pos, wp, tb.mv[cu]);
+    else move_ue<SCN>(pos, wp, kp);
+  }
 
   // ---- 2. association: closest BS with snr > snr_tr <=> d2 <= d2max (base.py:236-241)
   int srv = -1;
@@ -1013,8 +1021,10 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
       }
     } else {
+      // (heterogeneous entities: the map of this UE's class, [NU][H][W])
       const int xi = min(max(pos.x, 0), KPS(W) - 1), yi = min(max(pos.y, 0), KPS(H) - 1);
-      const int4 r = at(const_cast<int4*>(tb.assoc), 16u * (uint32_t)(yi * KPS(W) + xi));
+      const uint32_t moff = het ? (uint32_t)cu * (uint32_t)(KPS(W) * KPS(H)) : 0u;
+      const int4 r = at(const_cast<int4*>(tb.assoc), 16u * ((uint32_t)(yi * KPS(W) + xi) + moff));
       if (active) {
         srv = r.x;
         full = __hiloint2double(r.w, r.z);
@@ -2816,6 +2826,38 @@ __global__ void k_assoc_map(const int2* __restrict__ bs, int B, int W, int H, in
   map[i] = r;
 }
 
+// Heterogeneous entities, shared layout: one association map per UE class cu, [NU][H][W]. The
+// serving station of a UE of class cu at (x, y) is the closest station j (ties: lower index)
+// among those it can connect to, d2 <= d2max of the pair (class of j, cu) (base.py:236-241
+// with the pair's SNR, channels.py:133-146); the full rate is that pair's table at d2.
+__global__ void k_assoc_map_het(const int2* __restrict__ bs, int B, int W, int H,
+                                const uint8_t* __restrict__ bs_cls, const int2* __restrict__ pair,
+                                int NU, const double* __restrict__ rate_full,
+                                int4* __restrict__ map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int cells = W * H;
+  if (i >= cells * NU) return;
+  const int cu = i / cells, cell = i - cu * cells;
+  const int x = cell % W, y = cell / W;
+  long long best = LLONG_MAX;
+  int jb = -1;
+  for (int j = 0; j < B; ++j) {
+    const int2 q = bs[j];
+    const long long dx = (long long)x - q.x, dy = (long long)y - q.y;
+    const long long d2 = dx * dx + dy * dy;
+    if (d2 < best && d2 <= (long long)pair[(int)bs_cls[j] * NU + cu].y) {
+      best = d2;
+      jb = j;
+    }
+  }
+  int4 r = make_int4(-1, 0, 0, 0);
+  if (jb >= 0) {
+    const double f = rate_full[pair[(int)bs_cls[jb] * NU + cu].x + best];
+    r = make_int4(jb, (int)best, __double2loint(f), __double2hiint(f));
+  }
+  map[i] = r;
+}
+
 // Compact association tables (KTables::lds_blob), layout part: the serving station of every
 // cell from the association map as 4 bits (15 = none), and the station coordinates. One thread
 // per byte of the cell map (two cells).
@@ -2998,6 +3040,8 @@ struct mev_ctx {
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
   int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
+  int het_packed;     // heterogeneous entities on the packed kernels (U <= 64, shared layout;
+                      // one association map per UE class), else the block kernel
   // heterogeneous entities (build_het)
   uint8_t* h_bcl;
   uint8_t* h_ucl;
@@ -3629,8 +3673,10 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   // ---- association map of a shared layout (filled by mev_reset / mev_update_stations;
   //      <= 1024 x 1024 x 16 B)
   c->assoc = nullptr;
-  if (!params->bs_per_env && !c->kp.het) {
-    const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height;
+  c->het_packed = c->kp.het && params->num_ues <= 64 && !params->bs_per_env;
+  if (!params->bs_per_env && (!c->kp.het || c->het_packed)) {
+    const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height *
+                         (size_t)(c->het_packed ? c->kp.nu_cls : 1);
     if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
       return MEV_ENOMEM;
     }
@@ -3725,6 +3771,11 @@ void mev_destroy(mev_ctx* c) {
 int mev_d2max(const mev_ctx* c) { return c ? c->d2max : MEV_EINVAL; }
 
 int mev_launch_parts(const mev_ctx* c) { return c ? c->parts : MEV_EINVAL; }
+
+int mev_step_shape(const mev_ctx* c) {
+  if (!c) return MEV_EINVAL;
+  return c->kp.U <= 64 && (!c->kp.het || c->het_packed) ? 1 : 2;
+}
 
 int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EINVAL; }
 
@@ -4003,7 +4054,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   to_kernel(st, out, ks, ko);
   const KTables tb = tables_of(c);
   const KParams& kp = c->kp;
-  if (kp.U <= 64 && !kp.het) {
+  if (kp.U <= 64 && (!kp.het || c->het_packed)) {
     const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
     if (RESET) {
       const dim3 grid((unsigned)((groups + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -4024,8 +4075,17 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
 
 int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   if (!c || !bs_xy) return MEV_EINVAL;
-  if (c->p.bs_per_env || c->kp.het) return MEV_OK;  // the block kernel reads bs_xy itself
+  if (c->p.bs_per_env || (c->kp.het && !c->het_packed))
+    return MEV_OK;  // the block kernel reads bs_xy itself
   const int cells = c->p.width * c->p.height;
+  if (c->het_packed) {  // one map per UE class
+    const int n = cells * c->kp.nu_cls;
+    hipLaunchKernelGGL(k_assoc_map_het, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
+                       c->p.height, c->h_bcl, c->h_pair, c->kp.nu_cls, c->rate_full, c->assoc);
+    MEV_HIP(hipGetLastError());
+    return MEV_OK;
+  }
   hipLaunchKernelGGL(k_assoc_map, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
                      c->p.height, c->d2max, c->rate_full, c->assoc);
@@ -4105,7 +4165,7 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
     if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, (hipStream_t)stream));
     return MEV_OK;
   }
-  if (c->kp.U <= 64 && !c->kp.het)
+  if (c->kp.U <= 64 && (!c->kp.het || c->het_packed))
     return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
   return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
 }

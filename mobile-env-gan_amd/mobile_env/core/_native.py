@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -22,7 +22,7 @@ MEV_EHIP = -1000
 MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
-EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_lds_tables_bytes",
+EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations", "mev_build_rate_table", "mev_share_cents",
            "mev_rollout_instance", "mev_share_tie_free",
@@ -99,6 +99,8 @@ def lib():
         L.mev_d2max.restype = C.c_int
         L.mev_launch_parts.argtypes = [C.c_void_p]
         L.mev_launch_parts.restype = C.c_int
+        L.mev_step_shape.argtypes = [C.c_void_p]
+        L.mev_step_shape.restype = C.c_int
         L.mev_lds_tables_bytes.argtypes = [C.c_void_p]
         L.mev_lds_tables_bytes.restype = C.c_int
         L.mev_rate_table.argtypes = [C.c_void_p]

@@ -288,6 +288,12 @@ class StepEngine:
         return int(self._lib.mev_launch_parts(self._ctx))
 
     @property
+    def step_shape(self) -> str:
+        """"packed" (one lane per UE, several envs per wavefront) or "block" (one workgroup
+        per env) -- mev_step_shape."""
+        return {1: "packed", 2: "block"}[int(self._lib.mev_step_shape(self._ctx))]
+
+    @property
     def lds_tables_bytes(self) -> int:
         """Bytes of the LDS association tables of rollout launches (0: L2 map gather)."""
         return int(self._lib.mev_lds_tables_bytes(self._ctx))

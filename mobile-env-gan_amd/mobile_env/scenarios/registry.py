@@ -35,6 +35,23 @@ SCENARIOS["mobile-custom-128x1024-v0"] = dict(
     layout=None, mode="central", num_ues=1024, num_bs=128, velocity=10,
     per_env_layout=True)
 
+# mobile-large sizes and layout with heterogeneous entities (entities.py:7-22,33-45: every
+# station / UE carries its own parameters): three station classes {bw, freq, tx, height} and
+# three UE classes {velocity, snr_tr, noise, height}, station j in class j % 3, UE u in class
+# 7u % 3 -- the parameter mix of the reference fixture large_mixed (tests/golden/make_golden.py)
+SCENARIOS["mobile-large-mixed-v0"] = dict(
+    layout="large", mode="central", num_ues=LAYOUTS["large"]["num_ues"],
+    num_bs=len(LAYOUTS["large"]["bs"]), velocity=None, per_env_layout=False,
+    classes=dict(
+        bs_classes=[{"bw": 9e6, "freq": 2500, "tx": 40, "height": 50},
+                    {"bw": 9e6, "freq": 2500, "tx": 30, "height": 50},
+                    {"bw": 5e6, "freq": 1800, "tx": 35, "height": 30}],
+        ue_classes=[{"velocity": 1.5, "snr_tr": 2e-8, "noise": 1e-9, "height": 1.6},
+                    {"velocity": 10, "snr_tr": 2e-8, "noise": 1e-9, "height": 1.8},
+                    {"velocity": 3, "snr_tr": 1e-7, "noise": 2e-9, "height": 1.5}],
+        bs_class=[j % 3 for j in range(len(LAYOUTS["large"]["bs"]))],
+        ue_class=[(7 * u) % 3 for u in range(LAYOUTS["large"]["num_ues"])]))
+
 
 def spec(env_id: str) -> dict:
     if env_id not in SCENARIOS:

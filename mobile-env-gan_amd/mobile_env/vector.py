@@ -82,7 +82,8 @@ class VectorMobileEnv:
             ue={k: cfg["ue"][k] for k in ("snr_tr", "noise", "height")},
             util_lower=cfg["utility_params"]["lower"], util_upper=cfg["utility_params"]["upper"],
             util_coeffs=tuple(cfg["utility_params"]["coeffs"]),
-            stream_split=stream_split, fuse_steps=fuse_steps, **launch)
+            stream_split=stream_split, fuse_steps=fuse_steps,
+            **{k: v for k, v in (spec.get("classes") or {}).items()}, **launch)
         self.engine = StepEngine(p, bs_xy, self.seeds.numpy(), bs_count=bs_count, device=device,
                                  metrics=metrics, rate64=rate64, util64=util64)
         U = self.num_ues

@@ -165,13 +165,20 @@ class Core:
                 self.history[-1])
 
 
-def build(bs_xy, num_ues, seed, velocity, bs=None, ue=None, **kw):
+def build(bs_xy, num_ues, seed, velocity, bs=None, ue=None, classes=None, **kw):
+    """classes: heterogeneous entities (entities.py:7-22,33-45, every object its own
+    parameters) as {bs_classes, ue_classes, bs_class, ue_class} -- station j gets
+    bs_classes[bs_class[j]], UE u gets ue_classes[ue_class[u]] (velocity included)."""
     bs = bs or {"bw": 9e6, "freq": 2500, "tx": 40, "height": 50}
     ue = ue or {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
-    stations = [Station(i, int(x), int(y), bs["bw"], bs["freq"], bs["tx"], bs["height"])
-                for i, (x, y) in enumerate(bs_xy)]
-    devices = [Device(i, velocity, ue["snr_tr"], ue["noise"], ue["height"])
-               for i in range(num_ues)]
+    bsp = [classes["bs_classes"][classes["bs_class"][i]] if classes else bs
+           for i in range(len(bs_xy))]
+    uep = [classes["ue_classes"][classes["ue_class"][i]] if classes else dict(ue, velocity=velocity)
+           for i in range(num_ues)]
+    stations = [Station(i, int(x), int(y), q["bw"], q["freq"], q["tx"], q["height"])
+                for i, ((x, y), q) in enumerate(zip(bs_xy, bsp))]
+    devices = [Device(i, q["velocity"], q["snr_tr"], q["noise"], q["height"])
+               for i, q in enumerate(uep)]
     return Core(stations, devices, seed=seed, **kw)
 
 

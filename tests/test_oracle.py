@@ -180,6 +180,38 @@ def test_vec_oracle_matches_heterogeneous_fixture():
         np.testing.assert_array_equal(o["metrics"][:, :3], d["metrics"][:, s, :3])
 
 
+def test_port_matches_heterogeneous_fixture():
+    """The per-object port with per-entity parameters (port.build(classes=...), what bench.py's
+    cpu_baseline runs for mobile-large-mixed-v0) reproduces the reference's fixture."""
+    import json
+    d = load("large_mixed")
+    classes = dict(bs_classes=json.loads(str(d["bs_classes"])),
+                   ue_classes=json.loads(str(d["ue_classes"])),
+                   bs_class=d["bs_class"].tolist(), ue_class=d["ue_class"].tolist())
+    for k in range(len(d["seeds"])):
+        core = port.build(d["bs_xy"], d["xy"].shape[2], int(d["seeds"][k]), 0.0, classes=classes)
+        got = []
+        port.run_driver(core, 2, 20, on_step=lambda ep, s, c: got.append(c.snapshot()))
+        for s, (xy, srv, rate, util, met) in enumerate(got):
+            assert xy == [tuple(v) for v in d["xy"][k, s].tolist()]
+            assert srv == d["serving"][k, s].tolist()
+            assert rate == d["rate"][k, s].tolist()
+            np.testing.assert_array_equal(util, d["util"][k, s])
+
+
+def test_mixed_scenario_is_the_fixture_mix():
+    """mobile-large-mixed-v0 (the registered heterogeneous workload) carries the parameter
+    classes and class assignment of the reference fixture large_mixed, on the large layout."""
+    import json
+    from mobile_env.scenarios import registry
+    d = load("large_mixed")
+    c = registry.spec("mobile-large-mixed-v0")["classes"]
+    assert c["bs_classes"] == json.loads(str(d["bs_classes"]))
+    assert c["ue_classes"] == json.loads(str(d["ue_classes"]))
+    assert c["bs_class"] == d["bs_class"].tolist() and c["ue_class"] == d["ue_class"].tolist()
+    assert registry.LAYOUTS["large"]["bs"] == d["bs_xy"].tolist()
+
+
 def test_velocity_15_integer_step_matches_reference_expression():
     """The kernels' integer movement at velocity 1.5 (step_v15 in mev_step.hip: arrival at
     d2 <= 2; else per axis sgn(dx) [8 dx^2 > dy^2], and on an axis |step| 2 from an even
