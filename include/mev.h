@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 16
+#define MEV_ABI_VERSION 17
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -254,6 +254,16 @@ int mev_sync_stream_state(const mev_ctx* ctx, const mev_state* st, void* stream)
  * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the
  * shared layout between resets. No-op for per-env layouts. Stream-ordered. */
 int mev_update_stations(const mev_ctx* ctx, const int32_t* bs_xy, void* stream);
+
+/* Per-env station layouts (bs_per_env = 1): rebuild what the step kernels keep per env from
+ * bs_xy / bs_count for the envs with env_mask[e] (all if NULL) -- the block shape's station
+ * culling records (per map cell the stations that can be closest), which its short launches
+ * (mev_step, rollouts < 32 steps) read instead of scanning every station. Called by mev_reset;
+ * call it after changing an env's layout between resets. Envs whose records were never built
+ * are scanned in full (same results). No-op for shared layouts (mev_update_stations) and for
+ * the packed shape. Stream-ordered. */
+int mev_update_layouts(const mev_ctx* ctx, const mev_state* st, const uint8_t* env_mask,
+                       void* stream);
 
 /* Advance every env by `nsteps` steps of MComCore.step (base.py:230-296). An env whose
  * episode is over (t >= min(EP_MAX_TIME, departure)) is reset at the start of its next step

@@ -171,6 +171,10 @@ struct KTables {
   const int16_t* perm;      // [kp.bperm] stations grouped by class (segments of even length,
                             // padded with -1)
   const int* seg;           // [NB + 1] segment bounds in perm
+  // station culling records of per-env layouts kept across launches (mev_update_layouts):
+  // [E][cull_nc] 16-byte records (see block_cull_params), and per env 1 if they are valid
+  const unsigned char* crec_g;
+  const uint8_t* crec_ok;
 };
 
 // Element at a 32-bit byte offset from a wave-uniform base: addresses become
@@ -2263,6 +2267,15 @@ inline CullP block_cull_params(int B, int W, int H, bool het) {
   }
 }
 
+// The records kept in HBM for short launches (mev_update_layouts) use cells twice as wide (a
+// quarter of the records: 9.8 KB per env for 128 stations on 200 x 200, 3.2 candidates per cell
+// on average), since a one-step launch reads about one 64-byte line per UE of them.
+__host__ __device__ inline CullP pers_cull(int log, int W, int H) {
+  const int k = log + 1;
+  const int nx = (W + (1 << k) - 1) >> k, ny = (H + (1 << k) - 1) >> k;
+  return CullP{k, nx, nx * ny};
+}
+
 __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   BlockLds l;
   l.key = keys;
@@ -2291,6 +2304,60 @@ __device__ __forceinline__ int wave_isum(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, true);
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, true);
   return x;
+}
+
+// Station culling records (k_steps_block, k_cull_build): for every cell c of the map in squares
+// of 2^clog, rec[16 c] = {count, up to 15 candidate station indices}: s* = the station closest
+// to a point of the cell, D2 = its squared distance to the cell's farthest corner (every point
+// of the cell has a station within D2), and every station s whose squared distance to the cell
+// is <= D2. A station outside the list is farther than D2 from every point of the cell, so
+// strictly farther than s*: the minimum key over the list (ties by index included) is the
+// minimum over all stations. More than 15 candidates: count 255, the lane scans every station.
+// keys: the env's scaled station keys in LDS (k_steps_block's form); threads tid, tid + nt, ...
+__device__ void cull_cells(const int2* keys, int nb, int clog, int cnx, int cnc, int W, int H,
+                           int tid, int nt, unsigned char* rec_out) {
+  const v4u32* kk2 = reinterpret_cast<const v4u32*>(keys);
+  for (int c = tid; c < cnc; c += nt) {
+    const int cy = c / cnx, cx = c - cy * cnx;
+    const int x0 = cx << clog, y0 = cy << clog;
+    const int x1 = min(x0 + (1 << clog) - 1, W - 1);
+    const int y1 = min(y0 + (1 << clog) - 1, H - 1);
+    const int xm = (x0 + x1) >> 1, ym = (y0 + y1) >> 1;  // a point of the cell
+    const unsigned bk = scan_key_pairs(kk2, 0, nb >> 1, true, make_int2(xm, ym));
+    unsigned best = bk;
+    if (nb & 1) {
+      const int2 kv = keys[nb - 1];
+      const s16x2 p32 = {(short)(xm << 5), (short)(ym << 5)};
+      best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
+    }
+    const int2 ks = keys[best & ((1u << kKeyBits) - 1)];
+    const int sx = -(int)(short)(ks.x & 0xffff) >> 6, sy = -(int)(short)(ks.x >> 16) >> 6;
+    const int fx = max(sx - x0, x1 - sx), fy = max(sy - y0, y1 - sy);
+    const int D2 = fx * fx + fy * fy;
+    // the record's 16 bytes in four registers (byte p of word p / 4; no private array)
+    unsigned w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    auto put = [&](int p, unsigned v) {
+      const unsigned m = v << (8 * (p & 3));
+      w0 |= p < 4 ? m : 0u;
+      w1 |= (p >= 4 && p < 8) ? m : 0u;
+      w2 |= (p >= 8 && p < 12) ? m : 0u;
+      w3 |= p >= 12 ? m : 0u;
+    };
+    int n = 0;
+    for (int j = 0; j < nb; ++j) {
+      const int2 kv = keys[j];
+      const int qx = -(int)(short)(kv.x & 0xffff) >> 6, qy = -(int)(short)(kv.x >> 16) >> 6;
+      const int dx = max(max(x0 - qx, qx - x1), 0), dy = max(max(y0 - qy, qy - y1), 0);
+      if (dx * dx + dy * dy <= D2) {
+        if (n < 15) put(1 + n, (unsigned)j);
+        ++n;
+      }
+    }
+    for (int j = n; j < 15; ++j) put(1 + j, (unsigned)nb);
+    put(0, (unsigned)(n > 15 ? 255 : n));
+    const v4u32 w = {w0, w1, w2, w3};
+    *reinterpret_cast<v4u32*>(rec_out + 16 * c) = w;
+  }
 }
 
 // The env's steps i0 .. nsteps-1 for one workgroup (block shape); see k_steps_block.
@@ -2351,7 +2418,7 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
 }
 
 // nsteps steps of MComCore.step (base.py:230-296) for U > 64: one workgroup of ceil(U/64)
-// waves per env (lane u = UE u), envs e = blockIdx.x, blockIdx.x + gridDim.x, ...; each env's
+// waves per env (lane u = UE u), env e = blockIdx.x (grid = E); each env's
 // state stays in registers / LDS for the launch (loaded once, stored once) and every step's
 // outputs go to row i of the trajectory (traj) or over the previous step's. Per step, ONE
 // workgroup barrier:
@@ -2396,7 +2463,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
   const MoveP mp = HET ? tb.mv[cu]
                        : MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)};
-  for (int e = blockIdx.x; e < kp.E; e += gridDim.x) {
+  // one workgroup per env (grid = E): no loop over envs, whose loop-invariant values the
+  // compiler would hoist and spill under the 64-VGPR budget (76 B of scratch per lane, written
+  // by every wave at its start: 80 MB per launch at 1,024 envs of 1,024 UEs)
+  {
+    const int e = blockIdx.x;
+    if (e >= kp.E) return;
     // ---- prologue: state, stream, station keys, draw table -------------------------------
     const size_t idx = (size_t)e * U + u;
     int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
@@ -2418,12 +2490,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // ((|p - q|^2 - |p|^2 + 2^21) << 10) | j; otherwise m = -2 q, key = (dot2(p, m) << 10) + c
     const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * KPS(B) : st.bs_xy;
     bool in512 = true;
+    int2 q_own = make_int2(0, 0);  // station u (kept for its key below: no second load)
     for (int i = u; i < nb; i += blockDim.x) {
       const int2 qq = bsx[i];
+      if (i == u) q_own = qq;
       in512 = in512 && qq.x >= 0 && qq.y >= 0 && qq.x < 512 && qq.y < 512;
     }
+    // the episode draw table in LDS: all M pairs for launches of several steps; a one-step
+    // launch copies only the window it can use, 2U pairs from `tb` = 0 (a reset this step: the
+    // U initial positions, then the draws) or from `drawn` (the draws: at most U)
+    const int tb0 = nsteps == 1 ? (t >= KPS(t_end) ? 0 : drawn) : 0;
+    const int tlim = nsteps == 1 ? min(M, tb0 + 2 * U) : M;
     if (M)
-      for (int k = u; k < M; k += blockDim.x) L.tab[k] = tb.tab_xy[(size_t)e * M + k];
+      for (int k = tb0 + u; k < tlim; k += blockDim.x) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
+    auto tab_at = [&](int k) { return L.tab[k - tb0]; };  // (k < tlim wherever it is read)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
     // and stations beyond the env's count get the key that never wins, m = 0, c = UINT_MAX)
@@ -2434,7 +2514,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         lds_keys[k] = make_int2(0, -1);
         continue;
       }
-      const int2 qq = bsx[i];
+      const int2 qq = !HET && k == u ? q_own : bsx[i];
       const int f = scaled ? -64 : -2;
       const s16x2 m2 = {(short)(f * qq.x), (short)(f * qq.y)};
       lds_keys[k] = make_int2(__builtin_bit_cast(int, m2),
@@ -2460,47 +2540,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     };
     ahead_counts(t, wp, L.wt);
     __syncthreads();
-    // (uniform; launches of >= 32 steps: the records cost about as much as 18 steps' full scans)
-    const bool cull = CULL && scaled && nb > 0 && nsteps >= 32;
-    if (cull) {
-      // Candidates of cell C = [x0, x1] x [y0, y1]: s* = the station closest to a point of C,
-      // D2 = its squared distance to C's farthest corner (every point of C has a station
-      // within D2), and every station s whose squared distance to C is <= D2. A station
-      // outside the list is farther than D2 from every point of C, so strictly farther than
-      // s*: the minimum key over the list (ties by index included) is the minimum over all
-      // stations. More than 15 candidates: count 255, the lane scans every station.
-      const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
-      for (int c = u; c < CNC; c += blockDim.x) {
-        const int cy = c / CNX, cx = c - cy * CNX;
-        const int x0 = cx << CLOG, y0 = cy << CLOG;
-        const int x1 = min(x0 + (1 << CLOG) - 1, KPS(W) - 1);
-        const int y1 = min(y0 + (1 << CLOG) - 1, KPS(H) - 1);
-        const int xm = (x0 + x1) >> 1, ym = (y0 + y1) >> 1;  // a point of the cell
-        const unsigned bk = scan_key_pairs(kk2, 0, nb >> 1, true, make_int2(xm, ym));
-        unsigned best = bk;
-        if (nb & 1) {
-          const int2 kv = lds_keys[nb - 1];
-          const s16x2 p32 = {(short)(xm << 5), (short)(ym << 5)};
-          best = min(best, (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false));
-        }
-        const int2 ks = lds_keys[best & ((1u << kKeyBits) - 1)];
-        const int sx = -(int)(short)(ks.x & 0xffff) >> 6, sy = -(int)(short)(ks.x >> 16) >> 6;
-        const int fx = max(sx - x0, x1 - sx), fy = max(sy - y0, y1 - sy);
-        const int D2 = fx * fx + fy * fy;
-        unsigned char* r = crec + 16 * c;
-        int n = 0;
-        for (int j = 0; j < nb; ++j) {
-          const int2 kv = lds_keys[j];
-          const int qx = -(int)(short)(kv.x & 0xffff) >> 6, qy = -(int)(short)(kv.x >> 16) >> 6;
-          const int dx = max(max(x0 - qx, qx - x1), 0), dy = max(max(y0 - qy, qy - y1), 0);
-          if (dx * dx + dy * dy <= D2) {
-            if (n < 15) r[1 + n] = (unsigned char)j;
-            ++n;
-          }
-        }
-        for (int j = n; j < 15; ++j) r[1 + j] = (unsigned char)nb;
-        r[0] = (unsigned char)(n > 15 ? 255 : n);
-      }
+    // (uniform) launches of >= 32 steps build the records in LDS (they cost about as much as
+    // 18 steps' full scans); shorter ones read the env's records kept in HBM by
+    // mev_update_layouts, where they are valid for its layout
+    const bool pers = CULL && tb.crec_g != nullptr && nsteps < 32;
+    const int erec = PER_ENV_BS ? e : 0;  // (a shared layout: one record set)
+    const bool cull = CULL && scaled && nb > 0 && (pers ? tb.crec_ok[erec] != 0 : nsteps >= 32);
+    const CullP pc = pers_cull(CLOG, KPS(W), KPS(H));
+    const int RLOG = pers ? pc.log : CLOG, RNX = pers ? pc.nx : CNX, RNC = pers ? pc.nc : CNC;
+    const unsigned char* const grec = pers ? tb.crec_g + (size_t)erec * pc.nc * 16 : nullptr;
+    if (cull && !pers) {
+      cull_cells(lds_keys, nb, CLOG, CNX, CNC, KPS(W), KPS(H), u, blockDim.x, crec);
       __syncthreads();
     }
 
@@ -2520,7 +2570,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         wp = make_int2(-1, -1);
         if (M) {
           if (valid) {
-            const int p = L.tab[u];
+            const int p = tab_at(u);
             pos = make_int2((int)(short)p, p >> 16);
           }
           drawn = U;
@@ -2560,7 +2610,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int k = drawn + rank;  // pair index in the episode
         if (M && drawn + tot <= M) {  // every pair precomputed (the common case)
           if (need) {
-            const int p = L.tab[k];
+            const int p = tab_at(k);
             wp = make_int2((int)(short)p, p >> 16);
           }
           s_ok = false;
@@ -2584,7 +2634,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           if (need) {
             u128 s_fin;
             if (M && k < M) {
-              const int p = L.tab[k];
+              const int p = tab_at(k);
               wp = make_int2((int)(short)p, p >> 16);
               s_fin = base;
             } else {
@@ -2615,8 +2665,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // candidate (a per-lane ds_read_b64), until no lane of the wave has more
       bool full_scan = true;
       if (cull) {
-        const int cell = min(__mul24(max(pos.y, 0) >> CLOG, CNX) + (max(pos.x, 0) >> CLOG), CNC - 1);
-        const v4u32 rec = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
+        const int cell = min(__mul24(max(pos.y, 0) >> RLOG, RNX) + (max(pos.x, 0) >> RLOG), RNC - 1);
+        const v4u32 rec = pers ? *reinterpret_cast<const v4u32*>(grec + 16 * cell)
+                               : *reinterpret_cast<const v4u32*>(crec + 16 * cell);
         const int cn = active ? (int)(rec.x & 255u) : 0;
         full_scan = bal(cn > 15) != 0;
         if (!full_scan) {
@@ -2767,8 +2818,39 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             make_ulonglong2((uint64_t)sf, (uint64_t)(sf >> 64));
       }
     }
-    __syncthreads();  // LDS reused by the next env
   }
+}
+
+// Station culling records of per-env layouts (mev_update_layouts): one workgroup per env with
+// mask[e] (all if NULL), the env's scaled station keys in LDS as k_steps_block forms them, then
+// its records (cull_cells) to crec_g[e]; crec_ok[e] = 1 where k_steps_block would cull (every
+// station and the map inside 512 x 512, at least one station).
+// (A shared layout: one workgroup, one record set for every env.)
+__global__ __launch_bounds__(256) void k_cull_build(KParams kp, KState st,
+                                                    const uint8_t* __restrict__ mask,
+                                                    int per_env, unsigned char* __restrict__ crec_g,
+                                                    uint8_t* __restrict__ crec_ok) {
+  __shared__ __align__(16) int2 keys[kMaxB + 2];
+  const int e = blockIdx.x;
+  if (e >= kp.E || (mask != nullptr && !mask[e])) return;
+  const int t = threadIdx.x;
+  const int nb = per_env && st.bs_count ? st.bs_count[e] : kp.B;
+  const int2* bsx = st.bs_xy + (per_env ? (size_t)e * kp.B : 0);
+  bool in512 = true;
+  for (int i = t; i < nb; i += blockDim.x) {
+    const int2 q = bsx[i];
+    in512 = in512 && q.x >= 0 && q.y >= 0 && q.x < 512 && q.y < 512;
+    const s16x2 m2 = {(short)(-64 * q.x), (short)(-64 * q.y)};
+    keys[i] = make_int2(__builtin_bit_cast(int, m2),
+                        (int)(((unsigned)(q.x * q.x + q.y * q.y + (1 << 21)) << kKeyBits) | (unsigned)i));
+  }
+  if (t == 0) keys[nb] = make_int2(0, -1);
+  const bool ok = __syncthreads_and(in512) && kp.W <= 512 && kp.H <= 512 && nb > 0;
+  if (t == 0) crec_ok[e] = ok ? 1 : 0;
+  if (!ok) return;
+  const CullP pc = pers_cull(kp.cull_log, kp.W, kp.H);
+  cull_cells(keys, nb, pc.log, pc.nx, pc.nc, kp.W, kp.H, t, blockDim.x,
+             crec_g + (size_t)e * pc.nc * 16);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3040,6 +3122,8 @@ struct mev_ctx {
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
   int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
+  unsigned char* crec_g;  // per-env layouts, block shape: culling records kept in HBM
+  uint8_t* crec_ok;       // (mev_update_layouts; KTables::crec_g)
   int het_packed;     // heterogeneous entities on the packed kernels (U <= 64, shared layout;
                       // one association map per UE class), else the block kernel
   // heterogeneous entities (build_het)
@@ -3538,6 +3622,8 @@ static KTables tables_of(const mev_ctx* c) {
   tb.mv = c->h_mv;
   tb.perm = c->h_perm;
   tb.seg = c->h_seg;
+  tb.crec_g = c->crec_g;
+  tb.crec_ok = c->crec_ok;
   return tb;
 }
 
@@ -3682,6 +3768,19 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     }
     MEV_HIP(hipMemset(c->assoc, 0xff, bytes));  // srv -1 everywhere until a layout is set
   }
+  // ---- culling records of the block kernel kept in HBM (mev_update_layouts /
+  //      mev_update_stations; one set per env, or one for a shared layout), <= 2 GiB
+  c->crec_g = nullptr;
+  c->crec_ok = nullptr;
+  if (c->kp.U > 64 && c->kp.cull_nc > 0 && !c->kp.het) {
+    const size_t n = params->bs_per_env ? (size_t)params->num_envs : 1;
+    const size_t bytes = n * (size_t)pers_cull(c->kp.cull_log, c->kp.W, c->kp.H).nc * 16;
+    if (bytes <= ((size_t)2 << 30)) {
+      if (hipMalloc(&c->crec_g, bytes) != hipSuccess || hipMalloc(&c->crec_ok, n) != hipSuccess)
+        return MEV_ENOMEM;
+      MEV_HIP(hipMemset(c->crec_ok, 0, n));  // none valid until built
+    }
+  }
   if (!c->kp.het) {  // LDS tables: shared layouts (modes 1-3), per-env layouts (mode 4)
     rc = build_lds_tables(c);
     if (rc) {
@@ -3752,6 +3851,8 @@ void mev_destroy(mev_ctx* c) {
   (void)hipFree(c->jump);
   if (c->util) (void)hipFree(c->util);
   if (c->assoc) (void)hipFree(c->assoc);
+  if (c->crec_g) (void)hipFree(c->crec_g);
+  if (c->crec_ok) (void)hipFree(c->crec_ok);
   if (c->blob) (void)hipFree(c->blob);
   if (c->rankw) (void)hipFree(c->rankw);
   if (c->dwords) (void)hipFree(c->dwords);
@@ -4077,6 +4178,13 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
   if (!c || !bs_xy) return MEV_EINVAL;
   if (c->p.bs_per_env || (c->kp.het && !c->het_packed))
     return MEV_OK;  // the block kernel reads bs_xy itself
+  if (c->crec_g) {  // (shared layout, block shape) the culling records of the layout
+    KState ks{};
+    ks.bs_xy = reinterpret_cast<const int2*>(bs_xy);
+    hipLaunchKernelGGL(k_cull_build, dim3(1), dim3(256), 0, (hipStream_t)stream, c->kp, ks,
+                       nullptr, 0, c->crec_g, c->crec_ok);
+    MEV_HIP(hipGetLastError());
+  }
   const int cells = c->p.width * c->p.height;
   if (c->het_packed) {  // one map per UE class
     const int n = cells * c->kp.nu_cls;
@@ -4109,6 +4217,20 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        c->kp.lds_r16_off, c->rankw);
     MEV_HIP(hipGetLastError());
   }
+  return MEV_OK;
+}
+
+int mev_update_layouts(const mev_ctx* c, const mev_state* st, const uint8_t* env_mask,
+                       void* stream) {
+  if (!c || !st || !st->bs_xy) return MEV_EINVAL;
+  if (!c->p.bs_per_env || !c->crec_g) return MEV_OK;  // nothing kept per env
+  KState ks;
+  KOut ko{};
+  mev_outputs none{};
+  to_kernel(st, &none, ks, ko);
+  hipLaunchKernelGGL(k_cull_build, dim3((unsigned)c->kp.E), dim3(256), 0, (hipStream_t)stream,
+                     c->kp, ks, env_mask, 1, c->crec_g, c->crec_ok);
+  MEV_HIP(hipGetLastError());
   return MEV_OK;
 }
 
@@ -4145,6 +4267,8 @@ int mev_reset(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   int rc = check_bufs(c, st, out);
   if (rc) return rc;
   rc = mev_update_stations(c, st->bs_xy, stream);
+  if (rc) return rc;
+  rc = mev_update_layouts(c, st, env_mask, stream);
   if (rc) return rc;
   rc = mev_prepare_draws(c, st, env_mask, stream);
   if (rc) return rc;

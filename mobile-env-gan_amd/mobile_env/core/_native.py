@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -24,7 +24,7 @@ MEV_ECHANNEL = -1001
 # every symbol include/mev.h declares (tests check the library exports all of them)
 EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
-           "mev_update_stations", "mev_build_rate_table", "mev_share_cents",
+           "mev_update_stations", "mev_update_layouts", "mev_build_rate_table", "mev_share_cents",
            "mev_rollout_instance", "mev_share_tie_free",
            "mev_reset", "mev_prepare_draws", "mev_sync_stream_state", "mev_step", "mev_rollout", "mev_rollout_timed", "mev_strerror", "mev_last_hip_error")
 
@@ -117,6 +117,8 @@ def lib():
         L.mev_sync_stream_state.restype = C.c_int
         L.mev_update_stations.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mev_update_stations.restype = C.c_int
+        L.mev_update_layouts.argtypes = [C.c_void_p, C.POINTER(MevState), C.c_void_p, C.c_void_p]
+        L.mev_update_layouts.restype = C.c_int
         L.mev_reset.argtypes = [C.c_void_p, C.POINTER(MevState), C.POINTER(MevOutputs),
                                 C.c_void_p, C.c_void_p]
         L.mev_reset.restype = C.c_int

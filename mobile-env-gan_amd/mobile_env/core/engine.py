@@ -251,6 +251,8 @@ class StepEngine:
         with torch.cuda.device(device):
             N.check(L.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),
                     "mev_update_stations")
+            N.check(L.mev_update_layouts(self._ctx, C.byref(self._st), None, self._stream()),
+                    "mev_update_layouts")
 
     # -- plumbing -----------------------------------------------------------------------------
     def _bind(self):
@@ -364,14 +366,16 @@ class StepEngine:
         if tuple(bs.shape) != tuple(self.bs_xy.shape):
             raise ValueError("layout shape mismatch")
         _check_station_range(bs, bs_count)
+        if bs_count is not None and self.bs_count is None:
+            raise ValueError("engine was built without bs_count")
         self.bs_xy.copy_(bs)
-        with torch.cuda.device(self.device):  # shared layout: re-derive the station keys
+        if bs_count is not None:
+            self.bs_count.copy_(torch.as_tensor(bs_count, dtype=torch.int32))
+        with torch.cuda.device(self.device):  # re-derive the station keys / culling records
             N.check(self._lib.mev_update_stations(self._ctx, _ptr(self.bs_xy), self._stream()),
                     "mev_update_stations")
-        if bs_count is not None:
-            if self.bs_count is None:
-                raise ValueError("engine was built without bs_count")
-            self.bs_count.copy_(torch.as_tensor(bs_count, dtype=torch.int32))
+            N.check(self._lib.mev_update_layouts(self._ctx, C.byref(self._st), None,
+                                                 self._stream()), "mev_update_layouts")
 
     def reset(self, mask=None):
         """MComCore.reset for all envs (mask None) or envs where mask[e] != 0."""
