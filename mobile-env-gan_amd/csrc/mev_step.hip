@@ -2314,7 +2314,7 @@ __device__ __forceinline__ int wave_isum(int x) {
 // strictly farther than s*: the minimum key over the list (ties by index included) is the
 // minimum over all stations. More than 15 candidates: count 255, the lane scans every station.
 // keys: the env's scaled station keys in LDS (k_steps_block's form); threads tid, tid + nt, ...
-__device__ void cull_cells(const int2* keys, int nb, int clog, int cnx, int cnc, int W, int H,
+__device__ __forceinline__ void cull_cells(const int2* keys, int nb, int clog, int cnx, int cnc, int W, int H,
                            int tid, int nt, unsigned char* rec_out) {
   const v4u32* kk2 = reinterpret_cast<const v4u32*>(keys);
   for (int c = tid; c < cnc; c += nt) {
@@ -2334,29 +2334,19 @@ __device__ void cull_cells(const int2* keys, int nb, int clog, int cnx, int cnc,
     const int sx = -(int)(short)(ks.x & 0xffff) >> 6, sy = -(int)(short)(ks.x >> 16) >> 6;
     const int fx = max(sx - x0, x1 - sx), fy = max(sy - y0, y1 - sy);
     const int D2 = fx * fx + fy * fy;
-    // the record's 16 bytes in four registers (byte p of word p / 4; no private array)
-    unsigned w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    auto put = [&](int p, unsigned v) {
-      const unsigned m = v << (8 * (p & 3));
-      w0 |= p < 4 ? m : 0u;
-      w1 |= (p >= 4 && p < 8) ? m : 0u;
-      w2 |= (p >= 8 && p < 12) ? m : 0u;
-      w3 |= p >= 12 ? m : 0u;
-    };
+    unsigned char* const r = rec_out + 16 * c;  // (byte stores: LDS in k_steps_block)
     int n = 0;
     for (int j = 0; j < nb; ++j) {
       const int2 kv = keys[j];
       const int qx = -(int)(short)(kv.x & 0xffff) >> 6, qy = -(int)(short)(kv.x >> 16) >> 6;
       const int dx = max(max(x0 - qx, qx - x1), 0), dy = max(max(y0 - qy, qy - y1), 0);
       if (dx * dx + dy * dy <= D2) {
-        if (n < 15) put(1 + n, (unsigned)j);
+        if (n < 15) r[1 + n] = (unsigned char)j;
         ++n;
       }
     }
-    for (int j = n; j < 15; ++j) put(1 + j, (unsigned)nb);
-    put(0, (unsigned)(n > 15 ? 255 : n));
-    const v4u32 w = {w0, w1, w2, w3};
-    *reinterpret_cast<v4u32*>(rec_out + 16 * c) = w;
+    for (int j = n; j < 15; ++j) r[1 + j] = (unsigned char)nb;
+    r[0] = (unsigned char)(n > 15 ? 255 : n);
   }
 }
 
