@@ -471,7 +471,10 @@ def main():
                           "rocprof_launch_ms": rp1,
                           "env_steps_per_s": E / (avg * 1e-3),
                           "basis": "SURVEY.md 8d canonical bytes per env-step x E, one-step "
-                                   "launch (make().step(), mev_step(1))"})
+                                   "launch (make().step(), mev_step(1))",
+                          "frac_basis": "canonical: frac counts SURVEY 8d's bytes, which the "
+                                        "launch does not all move (int16 state); "
+                                        "traffic_frac = the PMC bytes it moves / peak"})
 
     if rank == 0:
         value = world * E * K / elapsed

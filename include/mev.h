@@ -221,8 +221,8 @@ int mev_rollout_instance(const mev_ctx* ctx);
 /* 1 when the context's rate table needs no tie test in the ResourceFair share of the kernels
  * that form it from a 100/n table: for every entry and every share count n <= num_ues,
  * rint(full * fl(100 / n)) equals the reference's rint(fl(full / n) * 100) (checked
- * exhaustively at mev_create); the scenario-constant two-group and block kernels then skip the
- * test and its exact fallback. */
+ * exhaustively at mev_create when entries x num_ues <= 10^8; 0 beyond); the scenario-constant
+ * two-group and block kernels then skip the test and its exact fallback. */
 int mev_share_tie_free(const mev_ctx* ctx);
 
 /* Host helper: numpy-compatible seeding, np.random.default_rng(seed) ->

@@ -3212,6 +3212,9 @@ static unsigned fbits(float f) {
 // n), IEEE double on the host like the device's; a table that fails anywhere keeps the test.
 static bool share_tie_free(const double* full, int64_t n_d2, int nmax) {
   if (!full || n_d2 <= 0 || nmax < 1 || nmax > kMaxU) return false;
+  // (bounded host cost at mev_create: tables x counts beyond 10^8 pairs -- e.g. a 1024 x 1024
+  // map where every distance connects, with 1,024 UEs -- keep the tie test instead)
+  if ((double)n_d2 * (double)nmax > 1e8) return false;
   for (int n = 1; n <= nmax; ++n) {
     const double r100 = 100.0 / (double)n;
     for (int64_t d = 0; d < n_d2; ++d) {
@@ -4026,7 +4029,14 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       MEV_HIP(hipGetLastError());
       return MEV_OK;
     }
-    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && pairs >= c->lds2_wgs * kLds2Waves) {
+    // (two_groups > 0: also batches that do not fill the resident workgroups, with fewer
+    // waves per workgroup -- A/B switch)
+    const bool force2 = c->p.two_groups > 0;
+    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok &&
+        (pairs >= c->lds2_wgs * kLds2Waves || force2)) {
+      const int nw2 = pairs >= c->lds2_wgs * kLds2Waves
+                          ? kLds2Waves
+                          : std::max(1, std::min(kLds2Waves, (pairs + c->lds2_wgs - 1) / c->lds2_wgs));
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
       StepsKernel k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true>
@@ -4035,12 +4045,12 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                                   : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true>
                                                     : k_steps_lds2<30, 2>)
                                               : k_steps_lds2<30, 0>);
-      const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
+      const int blocks = std::min((pairs + nw2 - 1) / nw2, c->lds2_wgs);
       const int G = kp.envs_per_wave;
       const int srows = std::min(c->stage_rows2, nsteps);
-      const size_t sh = (size_t)kp.lds_assoc + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2) +
-                        (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
-      launch_k(k2, dim3(blocks), dim3(64 * kLds2Waves), sh, stream, ev, kp, ks, ko, tb, groups,
+      const size_t sh = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, 2) +
+                        (((size_t)srows * nw2 * G * 2 * 5 + 3) & ~(size_t)3);
+      launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
       return MEV_OK;

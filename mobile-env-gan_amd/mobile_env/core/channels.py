@@ -56,7 +56,20 @@ class Channel:
         """Full (unshared) rate at every connectable integer squared distance: float64
         [d2max + 1] with the connectable d2 exactly [0, d2max] (a prefix; checked over the
         map's squared distances, and over every station distance when the whole map range
-        connects). ``bs`` = {bw, freq, tx, height}, ``ue`` = {snr_tr, noise, height}."""
+        connects). ``bs`` = {bw, freq, tx, height}, ``ue`` = {snr_tr, noise, height}.
+        Memoised per parameter set (the scalar power per entry makes a table of every map
+        distance cost seconds; heterogeneous contexts ask for one per class pair)."""
+        key = (type(self), tuple(float(bs[k]) for k in ("bw", "freq", "tx", "height")),
+               tuple(float(ue[k]) for k in ("snr_tr", "noise", "height")), int(width),
+               int(height))
+        tab = _RATE_TABLES.get(key)
+        if tab is None:
+            tab = self._rate_table(bs, ue, width, height)
+            tab.setflags(write=False)
+            _RATE_TABLES[key] = tab
+        return tab.copy()
+
+    def _rate_table(self, bs: dict, ue: dict, width: int, height: int):
         map_hi = (width - 1) ** 2 + (height - 1) ** 2
         snr = self._snr_table(map_hi, bs, ue)
         conn = snr > ue["snr_tr"]
@@ -73,6 +86,9 @@ class Channel:
         # shapely's distance of integer points = sqrt(d2), correctly rounded
         distance = np.sqrt(np.arange(d2_hi + 1, dtype=np.float64))
         return self.snr_of_distance(distance, bs, ue)
+
+
+_RATE_TABLES: dict = {}  # Channel.rate_table's memo: (model, bs, ue, W, H) -> table
 
 
 class OkumuraHata(Channel):

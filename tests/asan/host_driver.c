@@ -1,7 +1,8 @@
 /* Host-code sanitizer driver (CPU test, tests/test_host.py::test_host_code_under_asan).
  *
- * Linked against a HOST-ONLY build of libmev.so (hipcc --offload-host-only, no device code)
- * compiled with -fsanitize=address,undefined, it calls every C-ABI entry point that does host
+ * Linked against libmev_asan.so (`make asan`: the host side compiled with
+ * -Xarch_host -fsanitize=address,undefined, the gfx950 device code built as usual and never
+ * launched here -- there is no GPU in the container), it calls every C-ABI entry point that does host
  * work without a GPU -- argument checks, numpy-compatible seeding, the libm channel table,
  * mev_create's validation and its failure path -- with buffers sized exactly, so an
  * out-of-bounds write or undefined behaviour in the host code aborts the run. Prints the seed
