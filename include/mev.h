@@ -133,7 +133,8 @@ typedef struct mev_params {
    *   lds_tables: rollouts of a shared layout read the association from LDS tables of mode
    *     1..3 (KTables::lds_blob in mev_step.hip), -1: from the L2 association map;
    *   two_groups: -1: one env group per wavefront in rollout launches (else two where the
-   *     batch fills the GPU with pairs);
+   *     batch fills the GPU with pairs); 1 / 2: the two-group kernel with two / one groups
+   *     per wavefront at any batch size;
    *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
    *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges);
    *   scenario_constants: -1: the generic kernel instances only (else a registered scenario's

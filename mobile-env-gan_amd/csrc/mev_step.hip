@@ -1988,11 +1988,12 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 
 // PE: per-env station layouts (KParams::lds_mode 4: the blob holds the rank index of S, 100/n
 // and rate_full over S; the env's station keys are staged per launch like k_steps_packed's)
-template <int UC, int SCN, bool PE = false, bool TF = false>
+// R = 2 env groups per wavefront; R = 1 (batches too small to fill the resident workgroups
+// with pairs: one group per wavefront, the same step code).
+template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
-  constexpr int R = 2;
   const int NW = (int)(blockDim.x >> 6);  // <= kLds2Waves
   constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC;
   const int NWG = NW * G * R;  // envs per workgroup tile
@@ -2012,7 +2013,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   int* ltab = lw + NW * R * G * (8 + KB + HS) + wv * R * G * M;
   int* srow = lw + NW * R * G * (8 + KB + HS + M);
   uint8_t* drow = reinterpret_cast<uint8_t*>(srow + stage_rows * NWG);
-  const int npairs = (ngroups + 1) / 2;
+  const int npairs = (ngroups + R - 1) / R;  // ("pairs": the wave's R groups)
   const int gstride = (int)gridDim.x * NW;
   const float lower = (float)kp.lower;
   const int pb0 = block_slot(kp.xcd_remap) * NW;
@@ -2044,11 +2045,11 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   // prefetched registers are never carried around a loop edge (a copy there would read them
   // before the loads land, tools/check_prefetch_regs.py). Every store between a prefetch and
   // its wait is unconditional -- the trajectory rows of every step, the state's buffer stores
-  // below -- so that 4 nsteps + 8 >= 64 of them make the wait free (vmcnt(63)).
+  // below -- so that 2R nsteps + 4R >= 64 of them make the wait free (vmcnt(63)).
   // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
   // halves (one barrier per flush), else the window cycles (two).
   const bool alt = 2 * nsteps <= stage_rows;
-  const bool saturated = 4 * nsteps + 8 >= 64;
+  const bool saturated = 2 * R * nsteps + 4 * R >= 64;  // (2R trajectory stores per step, 4R state)
   int hb = 0;  // the pair's first row slot (alt)
   const bool leader = m.u == PC - 1;
   const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
@@ -2067,7 +2068,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       bool env_ok[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int g = 2 * p + r;
+        const int g = R * p + r;
         e[r] = g * G + m.seg;
         env_ok[r] = (m.seg < G) && (e[r] < kp.E);
         nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
@@ -4029,27 +4030,39 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       MEV_HIP(hipGetLastError());
       return MEV_OK;
     }
-    // (two_groups > 0: also batches that do not fill the resident workgroups, with fewer
-    // waves per workgroup -- A/B switch)
-    const bool force2 = c->p.two_groups > 0;
-    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok &&
-        (pairs >= c->lds2_wgs * kLds2Waves || force2)) {
-      const int nw2 = pairs >= c->lds2_wgs * kLds2Waves
-                          ? kLds2Waves
-                          : std::max(1, std::min(kLds2Waves, (pairs + c->lds2_wgs - 1) / c->lds2_wgs));
+    // two groups per wavefront once the pairs fill every resident workgroup, else the
+    // one-group packed kernel below. mev_params.two_groups (A/B switches): -1 the packed kernel
+    // always; 1 / 2 this kernel with two / one groups per wavefront at any batch, as many
+    // waves per workgroup as fill the resident workgroups. Measured at 4,096 medium envs (1,024
+    // groups: one wave per SIMD either way): packed 129 us per 200-step launch, one group per
+    // wave here 136 us, two groups (two waves per CU) 230 us -- the step's dependency chain,
+    // not its instruction count, bounds a wave that is alone on its SIMD.
+    const int tg = c->p.two_groups;
+    const bool full2 = pairs >= c->lds2_wgs * kLds2Waves;
+    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2))) {
+      const int R = tg == 1 ? 2 : tg == 2 ? 1 : 2;
+      const int units = R == 2 ? pairs : groups;  // the waves' work units
+      const int nw2 = std::max(1, std::min(kLds2Waves, (units + c->lds2_wgs - 1) / c->lds2_wgs));
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
-      StepsKernel k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true>
-                                                    : k_steps_lds2<15, 1>)
-                                              : k_steps_lds2<15, 0>)
-                                  : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true>
-                                                    : k_steps_lds2<30, 2>)
-                                              : k_steps_lds2<30, 0>);
-      const int blocks = std::min((pairs + nw2 - 1) / nw2, c->lds2_wgs);
+      StepsKernel k2;
+      if (R == 2)
+        k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true> : k_steps_lds2<15, 1>)
+                                    : k_steps_lds2<15, 0>)
+                        : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true> : k_steps_lds2<30, 2>)
+                                    : k_steps_lds2<30, 0>);
+      else
+        k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true, 1>
+                                          : k_steps_lds2<15, 1, false, false, 1>)
+                                    : k_steps_lds2<15, 0, false, false, 1>)
+                        : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true, 1>
+                                          : k_steps_lds2<30, 2, false, false, 1>)
+                                    : k_steps_lds2<30, 0, false, false, 1>);
+      const int blocks = std::min((units + nw2 - 1) / nw2, c->lds2_wgs);
       const int G = kp.envs_per_wave;
       const int srows = std::min(c->stage_rows2, nsteps);
-      const size_t sh = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, 2) +
-                        (((size_t)srows * nw2 * G * 2 * 5 + 3) & ~(size_t)3);
+      const size_t sh = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R) +
+                        (((size_t)srows * nw2 * G * R * 5 + 3) & ~(size_t)3);
       launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
