@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 17
+#define MEV_ABI_VERSION 18
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -140,8 +140,13 @@ typedef struct mev_params {
    *   scenario_constants: -1: the generic kernel instances only (else a registered scenario's
    *     parameters are compiled in when every value matches);
    *   station_culling: -1: the U > 64 kernel scans every station per UE (else per-cell
-   *     candidate lists where the layout qualifies: 32..255 stations, map <= 512 x 512). */
+   *     candidate lists where the layout qualifies: 32..255 stations, map <= 512 x 512);
+   *   ues_per_lane: U > 64 kernel, 1 / 2 UEs per lane (0: two in one-step launches for
+   *     U > 512 with homogeneous entities -- half the waves per env, so that 1,024 envs of
+   *     1,024 UEs are resident in one round of the chip's wave slots instead of two -- and one
+   *     in multi-step launches). */
   int32_t lds_tables, two_groups, stage_rows, xcd_remap, scenario_constants, station_culling;
+  int32_t ues_per_lane;
 } mev_params;
 
 typedef struct mev_state {

@@ -2277,6 +2277,14 @@ __host__ __device__ inline CullP pers_cull(int log, int W, int H) {
   return CullP{k, nx, nx * ny};
 }
 
+// LDS bytes of k_steps_block's culling records: only launches of >= 32 steps build them in LDS
+// (shorter ones read the HBM records, or scan every station); with two UEs per lane in cells
+// twice as wide (pers_cull), so that four workgroups fit beside each other on a CU.
+inline size_t block_rec_bytes(const CullP& cp, int W, int H, int nsteps, int upl) {
+  if (cp.log <= 0 || nsteps < 32) return 0;
+  return 16 * (size_t)(upl == 2 ? pers_cull(cp.log, W, H).nc : cp.nc);
+}
+
 __device__ __forceinline__ BlockLds block_lds(char* base, int2* keys, int B) {
   BlockLds l;
   l.key = keys;
@@ -2429,29 +2437,45 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
 // barrier); the rare stream-state path (draws past the table, resets without one) takes an
 // extra barrier, block-uniform, before it writes the slot the other waves read at the step's
 // start.
-template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0, bool TF = false>
+// UPL UEs per lane (1, or 2 for U > 512: half the waves per env, so that a batch whose
+// one-UE-per-lane workgroups would take two rounds of the chip's resident waves fits in one):
+// the lane's UEs are tid + h * blockDim.x, h < UPL, and UE u belongs to the "virtual wave"
+// u >> 6 = w + h * nw -- the same partition of the env's UEs into 64-UE groups as with one UE
+// per lane, so that every per-wave count, scan and partial sum (and its summation order) is
+// the same.
+template <bool PER_ENV_BS, bool LEAN, bool HET, int SCN = 0, bool TF = false, int UPL = 1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_steps_block(
     KParams kp, KState st, KOut out, KTables tb, int nsteps, int traj) {
+  static_assert(UPL == 1 || (UPL == 2 && !HET), "two UEs per lane: homogeneous entities only");
   extern __shared__ __align__(16) char lds_raw[];
-  __shared__ __align__(16) int2 lds_keys[kMaxB + 2 + kMaxClasses];
-  const int u = threadIdx.x;
+  // (a scenario instance: its station count; LDS for four workgroups per CU with two UEs per lane)
+  __shared__ __align__(16) int2 lds_keys[SCN ? scn_const(SCN).B + 2 : kMaxB + 2 + kMaxClasses];
+  const int tid = threadIdx.x;
+  const int nt = blockDim.x;
   const int U = KPS(U);
-  const int lane = u & 63;
-  const int w = u >> 6;
-  const int nw = (blockDim.x + 63) >> 6;
-  const bool valid = u < U;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int nw = (nt + 63) >> 6;  // waves of the workgroup
+  const int nv = UPL * nw;        // virtual waves (<= 16: U <= 1024)
+  int uh[UPL];
+  bool valid[UPL];
+#pragma unroll
+  for (int h = 0; h < UPL; ++h) {
+    uh[h] = tid + h * nt;
+    valid[h] = uh[h] < U;
+  }
   const uint64_t lt = (1ull << lane) - 1ull;
   const int M = KPS(tab_m);
   const BlockLds L = block_lds(lds_raw, lds_keys, KPS(B), KPS(tab_m));
-  for (int n = u; n <= U; n += blockDim.x) L.r100[n] = n ? 100.0 / (double)n : 0.0;
+  for (int n = tid; n <= U; n += nt) L.r100[n] = n ? 100.0 / (double)n : 0.0;
   // station culling: per cell of the map, the stations that can be the closest to some point
   // of the cell (see the prologue)
   const bool CULL = !HET && KPS(cull_log) > 0;
   const int CLOG = KPS(cull_log), CNX = KPS(cull_nx), CNC = KPS(cull_nc);
   unsigned char* const crec =
       reinterpret_cast<unsigned char*>(lds_raw + block_lds_bytes(KPS(B), KPS(tab_m)));
-  // heterogeneous entities: this UE's class and movement parameters
-  const int cu = HET ? (valid ? (int)tb.ue_cls[u] : 0) : 0;
+  // heterogeneous entities (UPL 1): this UE's class and movement parameters
+  const int cu = HET ? (valid[0] ? (int)tb.ue_cls[tid] : 0) : 0;
   const MoveP mp = HET ? tb.mv[cu]
                        : MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)};
   // one workgroup per env (grid = E): no loop over envs, whose loop-invariant values the
@@ -2461,16 +2485,21 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int e = blockIdx.x;
     if (e >= kp.E) return;
     // ---- prologue: state, stream, station keys, draw table -------------------------------
-    const size_t idx = (size_t)e * U + u;
-    int2 pos = make_int2(0, 0), wp = make_int2(-1, -1);
-    if (valid) {
-      const int4 sv = load_ue(st.ue_state + idx);
-      pos = make_int2(sv.x, sv.y);
-      wp = make_int2(sv.z, sv.w);
+    const size_t ebase = (size_t)e * U;
+    int2 pos[UPL], wp[UPL];
+#pragma unroll
+    for (int h = 0; h < UPL; ++h) {
+      pos[h] = make_int2(0, 0);
+      wp[h] = make_int2(-1, -1);
+      if (valid[h]) {
+        const int4 sv = load_ue(st.ue_state + ebase + uh[h]);
+        pos[h] = make_int2(sv.x, sv.y);
+        wp[h] = make_int2(sv.z, sv.w);
+      }
     }
     int t = st.t[e];
     int drawn = M ? tb.drawn[e] : 0;
-    if (u == 0) {
+    if (tid == 0) {
       const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e);
       L.slot[0] = mk128(pr[0].x, pr[0].y);
       L.slot[1] = mk128(pr[1].x, pr[1].y);
@@ -2481,10 +2510,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // ((|p - q|^2 - |p|^2 + 2^21) << 10) | j; otherwise m = -2 q, key = (dot2(p, m) << 10) + c
     const int2* bsx = PER_ENV_BS ? st.bs_xy + (size_t)e * KPS(B) : st.bs_xy;
     bool in512 = true;
-    int2 q_own = make_int2(0, 0);  // station u (kept for its key below: no second load)
-    for (int i = u; i < nb; i += blockDim.x) {
+    int2 q_own = make_int2(0, 0);  // station tid (kept for its key below: no second load)
+    for (int i = tid; i < nb; i += nt) {
       const int2 qq = bsx[i];
-      if (i == u) q_own = qq;
+      if (i == tid) q_own = qq;
       in512 = in512 && qq.x >= 0 && qq.y >= 0 && qq.x < 512 && qq.y < 512;
     }
     // the episode draw table in LDS: all M pairs for launches of several steps; a one-step
@@ -2493,41 +2522,45 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int tb0 = nsteps == 1 ? (t >= KPS(t_end) ? 0 : drawn) : 0;
     const int tlim = nsteps == 1 ? min(M, tb0 + 2 * U) : M;
     if (M)
-      for (int k = tb0 + u; k < tlim; k += blockDim.x) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
+      for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
     auto tab_at = [&](int k) { return L.tab[k - tb0]; };  // (k < tlim wherever it is read)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
     // and stations beyond the env's count get the key that never wins, m = 0, c = UINT_MAX)
     const int nslot = HET ? kp.bperm : nb;
-    for (int k = u; k < nslot; k += blockDim.x) {
+    for (int k = tid; k < nslot; k += nt) {
       const int i = HET ? (int)tb.perm[k] : k;
       if (HET && (i < 0 || i >= nb)) {
         lds_keys[k] = make_int2(0, -1);
         continue;
       }
-      const int2 qq = !HET && k == u ? q_own : bsx[i];
+      const int2 qq = !HET && k == tid ? q_own : bsx[i];
       const int f = scaled ? -64 : -2;
       const s16x2 m2 = {(short)(f * qq.x), (short)(f * qq.y)};
       lds_keys[k] = make_int2(__builtin_bit_cast(int, m2),
                               (int)(((unsigned)(qq.x * qq.x + qq.y * qq.y + (1 << 21)) << kKeyBits) |
                                     (unsigned)i));
     }
-    for (int i = u; i < KPS(B); i += blockDim.x) L.cnt[i] = 0;  // step 0's counts
-    if (CULL && u == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
+    for (int i = tid; i < KPS(B); i += nt) L.cnt[i] = 0;  // step 0's counts
+    if (CULL && tid == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
     // the slot holds the state after the env's last draw: the state row without a table, or
     // after draws past it (mev_state.pcg)
     bool s_ok = !M || drawn > M;
     BlockRow prev{0, 0, 0};
-    // step 0's per-wave need / active counts (its lazy reset applied ahead)
-    auto ahead_counts = [&](int tn, int2 wpn, int* wt) {
+    // step 0's per-virtual-wave need / active counts (its lazy reset applied ahead)
+    auto ahead_counts = [&](int tn, const int2 (&wpn)[UPL], int* wt) {
       const bool rs = tn >= KPS(t_end);
       const int t0 = rs ? 0 : tn;
-      const bool act = valid && t0 >= KPS(arr_start) && t0 < KPS(arr_exit) &&
-                       (KPS(first_step_active) || t0 != 0);
-      const uint64_t mn = bal(act && (rs || wpn.x < 0)), ma = bal(act);
-      // {need, active} packed in one int (each <= 64 per wave, <= 1024 per env): one read
-      // and one scan per step
-      if (lane == 0) wt[w] = __popcll(mn) | (__popcll(ma) << 16);
+      const bool on = t0 >= KPS(arr_start) && t0 < KPS(arr_exit) &&
+                      (KPS(first_step_active) || t0 != 0);
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        const bool act = valid[h] && on;
+        const uint64_t mn = bal(act && (rs || wpn[h].x < 0)), ma = bal(act);
+        // {need, active} packed in one int (each <= 64 per wave, <= 1024 per env): one read
+        // and one scan per step
+        if (lane == 0) wt[w + h * nw] = __popcll(mn) | (__popcll(ma) << 16);
+      }
     };
     ahead_counts(t, wp, L.wt);
     __syncthreads();
@@ -2537,11 +2570,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const bool pers = CULL && tb.crec_g != nullptr && nsteps < 32;
     const int erec = PER_ENV_BS ? e : 0;  // (a shared layout: one record set)
     const bool cull = CULL && scaled && nb > 0 && (pers ? tb.crec_ok[erec] != 0 : nsteps >= 32);
+    // the records' cells: the HBM records' (twice as wide) for pers, and in LDS with two UEs per
+    // lane (a quarter of the LDS: four workgroups per CU, see block_rec_bytes)
     const CullP pc = pers_cull(CLOG, KPS(W), KPS(H));
-    const int RLOG = pers ? pc.log : CLOG, RNX = pers ? pc.nx : CNX, RNC = pers ? pc.nc : CNC;
+    const bool wide = pers || UPL == 2;
+    const int RLOG = wide ? pc.log : CLOG, RNX = wide ? pc.nx : CNX, RNC = wide ? pc.nc : CNC;
     const unsigned char* const grec = pers ? tb.crec_g + (size_t)erec * pc.nc * 16 : nullptr;
     if (cull && !pers) {
-      cull_cells(lds_keys, nb, CLOG, CNX, CNC, KPS(W), KPS(H), u, blockDim.x, crec);
+      cull_cells(lds_keys, nb, RLOG, RNX, RNC, KPS(W), KPS(H), tid, nt, crec);
       __syncthreads();
     }
 
@@ -2558,12 +2594,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       u128 base = 0, inc = 0;
       if (reset) {
         t = 0;
-        wp = make_int2(-1, -1);
+#pragma unroll
+        for (int h = 0; h < UPL; ++h) wp[h] = make_int2(-1, -1);
         if (M) {
-          if (valid) {
-            const int p = tab_at(u);
-            pos = make_int2((int)(short)p, p >> 16);
-          }
+#pragma unroll
+          for (int h = 0; h < UPL; ++h)
+            if (valid[h]) {
+              const int p = tab_at(uh[h]);
+              pos[h] = make_int2((int)(short)p, p >> 16);
+            }
           drawn = U;
           s_ok = false;
         } else {
@@ -2571,39 +2610,53 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           inc = L.slot[1];
           const ulonglong2 c = reinterpret_cast<const ulonglong2*>(st.pcg + (size_t)6 * e)[2];
           if (kp.movement_reseed) base = mk128(c.x, c.y);
-          if (valid) (void)pcg_draw_pair(base, inc, 2 * u, tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+#pragma unroll
+          for (int h = 0; h < UPL; ++h)
+            if (valid[h])
+              (void)pcg_draw_pair(base, inc, 2 * uh[h], tb.jump, kp.Wd, kp.Hd, pos[h].x, pos[h].y);
           koff = 2 * U;
           wait_vmem();
         }
       }
-      const bool active = valid && t >= KPS(arr_start) && t < KPS(arr_exit) &&
-                          (KPS(first_step_active) || t != 0);
-      const bool need = active && wp.x < 0;
-      const uint64_t mneed = bal(need);
+      const bool on = t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0);
+      bool active[UPL], need[UPL];
+      uint64_t mneed[UPL];
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        active[h] = valid[h] && on;
+        need[h] = active[h] && wp[h].x < 0;
+        mneed[h] = bal(need[h]);
+      }
 
-      const int scan_na = row_scan_i32(lane < nw ? wt[lane & 15] : 0);
-      const int pre_need = w ? (__builtin_amdgcn_readlane(scan_na, w - 1) & 0xffff) : 0;
-      const int tot_na = __builtin_amdgcn_readlane(scan_na, nw - 1);
+      const int scan_na = row_scan_i32(lane < nv ? wt[lane & 15] : 0);
+      const int tot_na = __builtin_amdgcn_readlane(scan_na, nv - 1);
       const int tot = tot_na & 0xffff;
       const int nact = tot_na >> 16;
       const int c3n = c3 == 2 ? 0 : c3 + 1;
       int* cnt_next = L.cnt + c3n * KPS(B);  // (last read in step i - 2)
-      if (SCN) {  // (a scenario instance: U >= B, one store per lane)
-        static_assert(!SCN || scn_const(SCN).U >= scn_const(SCN).B, "block scenario: U >= B");
-        if (u < KPS(B)) cnt_next[u] = 0;
+      if (SCN) {  // (a scenario instance: one store per lane)
+        static_assert(!SCN || scn_const(SCN).U / UPL >= scn_const(SCN).B, "block scenario: U >= UPL B");
+        if (tid < KPS(B)) cnt_next[tid] = 0;
       } else {
-        for (int k = u; k < KPS(B); k += blockDim.x) cnt_next[k] = 0;
+        for (int k = tid; k < KPS(B); k += nt) cnt_next[k] = 0;
       }
 
       // ---- B: waypoint draws in ue_id order (movement.py:44-47), move ------------------
-      const int rank = pre_need + (int)__popcll(mneed & lt);
+      int rank[UPL];
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        const int vw = w + h * nw;
+        const int pre_need = vw ? (__builtin_amdgcn_readlane(scan_na, vw - 1) & 0xffff) : 0;
+        rank[h] = pre_need + (int)__popcll(mneed[h] & lt);
+      }
       if (tot > 0) {
-        const int k = drawn + rank;  // pair index in the episode
         if (M && drawn + tot <= M) {  // every pair precomputed (the common case)
-          if (need) {
-            const int p = tab_at(k);
-            wp = make_int2((int)(short)p, p >> 16);
-          }
+#pragma unroll
+          for (int h = 0; h < UPL; ++h)
+            if (need[h]) {
+              const int p = tab_at(drawn + rank[h]);  // pair index in the episode
+              wp[h] = make_int2((int)(short)p, p >> 16);
+            }
           s_ok = false;
         } else {
           // beyond the table (or none): from the stream state after pair bidx - 1 (the slot,
@@ -2622,170 +2675,214 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             // compiler's vmcnt(0) there wait for the previous step's stores as well)
             wait_vmem();
           }
-          if (need) {
-            u128 s_fin;
-            if (M && k < M) {
-              const int p = tab_at(k);
-              wp = make_int2((int)(short)p, p >> 16);
-              s_fin = base;
-            } else {
-              s_fin = pcg_draw_pair(base, inc, koff + 2 * (k - bidx), tb.jump, kp.Wd, kp.Hd,
-                                    wp.x, wp.y);
+#pragma unroll
+          for (int h = 0; h < UPL; ++h)
+            if (need[h]) {
+              const int k = drawn + rank[h];
+              u128 s_fin;
+              if (M && k < M) {
+                const int p = tab_at(k);
+                wp[h] = make_int2((int)(short)p, p >> 16);
+                s_fin = base;
+              } else {
+                s_fin = pcg_draw_pair(base, inc, koff + 2 * (k - bidx), tb.jump, kp.Wd, kp.Hd,
+                                      wp[h].x, wp[h].y);
+              }
+              if (rank[h] == tot - 1) L.slot[0] = s_fin;  // the env's new stream state
             }
-            if (rank == tot - 1) L.slot[0] = s_fin;  // the env's new stream state
-          }
           s_ok = true;
         }
         drawn += tot;
       } else if (reset && !M) {  // reset without draws: after the initial pairs (uniform)
         __syncthreads();
-        if (u == U - 1)
-          L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos.x, pos.y);
+#pragma unroll
+        for (int h = 0; h < UPL; ++h)
+          if (uh[h] == U - 1)
+            L.slot[0] = pcg_draw_pair(base, inc, 2 * (U - 1), tb.jump, kp.Wd, kp.Hd, pos[h].x,
+                                      pos[h].y);
       }
-      if (active) move_ue_p(pos, wp, mp);
+#pragma unroll
+      for (int h = 0; h < UPL; ++h)
+        if (active[h]) move_ue_p(pos[h], wp[h], mp);
       ahead_counts(t + 1, wp, L.wt + 64 * (par ^ 1));  // the next step's, after this move
 
       // ---- association: min over the env's station keys (LDS broadcast reads) ----------
       // (ext_vector_type loads: one broadcast ds_read_b128 per two stations; HIP's int4 struct is
       // loaded member-wise, which became four ds_read2_b32 -- twice the LDS cycles)
       const v4u32* kk2 = reinterpret_cast<const v4u32*>(lds_keys);
-      unsigned best = UINT_MAX;
-      int srv = -1, d2s = 0;
-      double full = 0.0;
+      int srv[UPL];
+      double full[UPL];
+      unsigned best[UPL];
       // the cell's candidate list (CULL): its count and up to 15 station indices, one key per
-      // candidate (a per-lane ds_read_b64), until no lane of the wave has more
-      bool full_scan = true;
-      if (cull) {
-        const int cell = min(__mul24(max(pos.y, 0) >> RLOG, RNX) + (max(pos.x, 0) >> RLOG), RNC - 1);
-        const v4u32 rec = pers ? *reinterpret_cast<const v4u32*>(grec + 16 * cell)
-                               : *reinterpret_cast<const v4u32*>(crec + 16 * cell);
-        const int cn = active ? (int)(rec.x & 255u) : 0;
-        full_scan = bal(cn > 15) != 0;
-        if (!full_scan) {
-          const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
-          // the first four candidates unconditionally (four reads in flight; past a lane's
-          // count the record holds the padding index, whose key never wins), then one at a
-          // time while a lane of the wave has more (two at a time: timing-neutral)
-          auto key_of = [&](int j) {
-            const unsigned wd = j < 3 ? rec.x : j < 7 ? rec.y : j < 11 ? rec.z : rec.w;
-            const int2 kv = lds_keys[__builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u)];
-            return (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false);
-          };
-          best = min(min(key_of(0), key_of(1)), min(key_of(2), key_of(3)));
+      // candidate (a per-lane ds_read_b64), until no lane of the wave has more; with two UEs
+      // per lane both records are read, and both lists walked, together (one chain of reads,
+      // not two)
+      bool full_scan[UPL];
 #pragma unroll
-          for (int j = 4; j < 15; ++j) {
-            if (!bal(cn > j)) break;
-            best = min(best, key_of(j));
+      for (int h = 0; h < UPL; ++h) {
+        best[h] = UINT_MAX;
+        full_scan[h] = true;
+      }
+      if (cull) {
+        v4u32 rec[UPL];
+        int cn[UPL];
+        s16x2 p32[UPL];
+#pragma unroll
+        for (int h = 0; h < UPL; ++h) {
+          const int cell = min(__mul24(max(pos[h].y, 0) >> RLOG, RNX) + (max(pos[h].x, 0) >> RLOG),
+                               RNC - 1);
+          rec[h] = pers ? *reinterpret_cast<const v4u32*>(grec + 16 * cell)
+                        : *reinterpret_cast<const v4u32*>(crec + 16 * cell);
+        }
+#pragma unroll
+        for (int h = 0; h < UPL; ++h) {
+          cn[h] = active[h] ? (int)(rec[h].x & 255u) : 0;
+          full_scan[h] = bal(cn[h] > 15) != 0;
+          p32[h] = s16x2{(short)(pos[h].x << 5), (short)(pos[h].y << 5)};
+        }
+        // the first four candidates unconditionally (four reads in flight; past a lane's
+        // count the record holds the padding index, whose key never wins), then one at a
+        // time while a lane of the wave has more (two at a time: timing-neutral)
+        auto key_of = [&](int h, int j) {
+          const unsigned wd = j < 3 ? rec[h].x : j < 7 ? rec[h].y : j < 11 ? rec[h].z : rec[h].w;
+          const int2 kv = lds_keys[__builtin_amdgcn_ubfe(wd, (unsigned)(((j + 1) & 3) * 8), 8u)];
+          return (unsigned)__builtin_amdgcn_sdot2(p32[h], as_s16x2((unsigned)kv.x), kv.y, false);
+        };
+#pragma unroll
+        for (int h = 0; h < UPL; ++h)
+          if (!full_scan[h])
+            best[h] = min(min(key_of(h, 0), key_of(h, 1)), min(key_of(h, 2), key_of(h, 3)));
+#pragma unroll
+        for (int j = 4; j < 15; ++j) {
+          bool more = false;
+#pragma unroll
+          for (int h = 0; h < UPL; ++h) more = more || (!full_scan[h] && bal(cn[h] > j) != 0);
+          if (!more) break;
+#pragma unroll
+          for (int h = 0; h < UPL; ++h)
+            if (!full_scan[h]) best[h] = min(best[h], key_of(h, j));
+        }
+#pragma unroll
+        for (int h = 0; h < UPL; ++h)
+          if (!full_scan[h] && !active[h]) best[h] = UINT_MAX;
+      }
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        srv[h] = -1;
+        full[h] = 0.0;
+        int d2s = 0;
+        if (!HET) {
+          if (active[h] && full_scan[h]) {
+            best[h] = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos[h]);
+            if (nb & 1) {  // the odd last station
+              const int2 kv = lds_keys[nb - 1];
+              const s16x2 p32 = {(short)(pos[h].x << 5), (short)(pos[h].y << 5)};
+              const s16x2 pu = {(short)pos[h].x, (short)pos[h].y};
+              best[h] = min(best[h], scaled ? (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false)
+                                            : ((unsigned)__builtin_amdgcn_sdot2(pu, as_s16x2((unsigned)kv.x), 0, true) << kKeyBits) +
+                                                  (unsigned)kv.y);
+            }
           }
-          if (!active) best = UINT_MAX;
+          d2s = key_d2(best[h], pos[h]);
+          if (best[h] != UINT_MAX && d2s <= KPS(d2max)) srv[h] = (int)(best[h] & ((1u << kKeyBits) - 1));
+          full[h] = tb.rate_full[max(0, min(d2s, KPS(d2max)))];
+        } else {
+          // per station class: the class's closest station, connectable iff d2 <= d2max of the
+          // (station class, this UE's class) pair -- the closest connectable station overall is
+          // the smallest key among the connectable class minima (base.py:236-241)
+          if (active[h]) {
+            for (int c = 0; c < kp.nb_cls; ++c) {
+              const unsigned bc = scan_key_pairs(kk2, tb.seg[c] >> 1, tb.seg[c + 1] >> 1, scaled, pos[h]);
+              if (bc != UINT_MAX && key_d2(bc, pos[h]) <= tb.pair[c * kp.nu_cls + cu].y)
+                best[h] = min(best[h], bc);
+            }
+          }
+          d2s = key_d2(best[h], pos[h]);
+          if (best[h] != UINT_MAX) {
+            srv[h] = (int)(best[h] & ((1u << kKeyBits) - 1));
+            full[h] = tb.rate_full[tb.pair[(int)tb.bs_cls[srv[h]] * kp.nu_cls + cu].x + d2s];
+          }
         }
       }
-      if (!HET) {
-        if (active && full_scan) {
-          best = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos);
-          if (nb & 1) {  // the odd last station
-            const int2 kv = lds_keys[nb - 1];
-            const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
-            const s16x2 pu = {(short)pos.x, (short)pos.y};
-            best = min(best, scaled ? (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false)
-                                    : ((unsigned)__builtin_amdgcn_sdot2(pu, as_s16x2((unsigned)kv.x), 0, true) << kKeyBits) +
-                                          (unsigned)kv.y);
-          }
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        if (srv[h] >= 0) atomicAdd(&cnt[srv[h]], 1);
+        if (!LEAN) {
+          const int nc = __popcll(bal(srv[h] >= 0));  // (the ballot over the whole wavefront)
+          if (lane == 0) wt[32 + w + h * nw] = nc;
         }
-        d2s = key_d2(best, pos);
-        if (best != UINT_MAX && d2s <= KPS(d2max)) srv = (int)(best & ((1u << kKeyBits) - 1));
-        full = tb.rate_full[max(0, min(d2s, KPS(d2max)))];
-      } else {
-        // per station class: the class's closest station, connectable iff d2 <= d2max of the
-        // (station class, this UE's class) pair -- the closest connectable station overall is
-        // the smallest key among the connectable class minima (base.py:236-241)
-        if (active) {
-          for (int c = 0; c < kp.nb_cls; ++c) {
-            const unsigned bc = scan_key_pairs(kk2, tb.seg[c] >> 1, tb.seg[c + 1] >> 1, scaled, pos);
-            if (bc != UINT_MAX && key_d2(bc, pos) <= tb.pair[c * kp.nu_cls + cu].y)
-              best = min(best, bc);
-          }
-        }
-        d2s = key_d2(best, pos);
-        if (best != UINT_MAX) {
-          srv = (int)(best & ((1u << kKeyBits) - 1));
-          full = tb.rate_full[tb.pair[(int)tb.bs_cls[srv] * kp.nu_cls + cu].x + d2s];
-        }
-      }
-      if (srv >= 0) atomicAdd(&cnt[srv], 1);
-      if (!LEAN) {
-        const int nc = __popcll(bal(srv >= 0));  // (the ballot over the whole wavefront)
-        if (lane == 0) wt[32 + w] = nc;
       }
       __syncthreads();  // ---- the step's barrier
       // the rate gather is waited for here (after the barrier: its latency overlaps the wait for
       // the other waves), on every path, before this step's stores: a lane or wave that never
       // reads `full` would carry the load as pending to a later merge, whose vmcnt(0) (before
       // the register is reused) would then also wait for the stores
-      asm volatile("" ::"v"(full));
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) asm volatile("" ::"v"(full[h]));
 
       // ---- C: ResourceFair share + rounding, utility, stores, partial sums -------------
-      double cents = 0.0;
-      float cents_f = 0.f;
-      if (srv >= 0) {
-        const int n = cnt[srv];
-        if (TF) {  // tie-free table (share_tie_free): the product rounds like the reference
-          cents = rint(full * L.r100[n]);
-          cents_f = (float)cents;
+      // this env's rows in the output rows: a wave-uniform base and a 32-bit lane offset
+      const size_t rb = (size_t)row * kp.E * U + ebase;
+#pragma unroll
+      for (int h = 0; h < UPL; ++h) {
+        const int vw = w + h * nw;
+        double cents = 0.0;
+        float cents_f = 0.f;
+        if (srv[h] >= 0) {
+          const int n = cnt[srv[h]];
+          if (TF) {  // tie-free table (share_tie_free): the product rounds like the reference
+            cents = rint(full[h] * L.r100[n]);
+            cents_f = (float)cents;
+          } else {
+            cents = share_cents_r(full[h], L.r100[n], n, cents_f);
+          }
+        }
+        const bool exact_util = !LEAN;
+        const double rate = cents / 100.0;
+        double util = 0.0;
+        if (active[h])
+          util = exact_util ? utility_of(rate, cents, kp, tb.util)
+                            : utility_f32r<SCN>(cents_f, cents_f * 0.01f, kp);
+        if (valid[h]) {
+          at(out.serving + rb, 4u * (uint32_t)uh[h]) = srv[h];
+          at(out.obs + rb, 16u * (uint32_t)uh[h]) =
+              make_float4((float)pos[h].x * KPSF(inv_w), (float)pos[h].y * KPSF(inv_h),
+                          cents_f * 0.01f, (float)util);
+          if (!LEAN) {
+            if (out.rate64) out.rate64[rb + uh[h]] = rate;
+            if (out.util64) out.util64[rb + uh[h]] = active[h] ? util : __builtin_nan("");
+          }
+        }
+        if (LEAN) {  // 2^-24 fixed point: |sum| <= 64 * 2^24 (block_finish_row_lean)
+          const int isu = wave_isum((int)((float)util * 0x1p24f));  // (util = 0 where inactive)
+          if (lane == 63) ps[vw] = (double)isu;
         } else {
-          cents = share_cents_r(full, L.r100[n], n, cents_f);
-        }
-      }
-      const bool exact_util = !LEAN;
-      const double rate = cents / 100.0;
-      double util = 0.0;
-      if (active)
-        util = exact_util ? utility_of(rate, cents, kp, tb.util)
-                          : utility_f32r<SCN>(cents_f, cents_f * 0.01f, kp);
-      const size_t ro = (size_t)row * kp.E * U + idx;
-      if (valid) {
-        // this env's row in the output rows: a wave-uniform base and a 32-bit lane offset
-        const size_t rb = (size_t)row * kp.E * U + (size_t)e * U;
-        at(out.serving + rb, 4u * (uint32_t)u) = srv;
-        at(out.obs + rb, 16u * (uint32_t)u) =
-            make_float4((float)pos.x * KPSF(inv_w), (float)pos.y * KPSF(inv_h), cents_f * 0.01f,
-                        (float)util);
-        if (!LEAN) {
-          if (out.rate64) out.rate64[ro] = rate;
-          if (out.util64) out.util64[ro] = active ? util : __builtin_nan("");
-        }
-      }
-      if (LEAN) {  // 2^-24 fixed point: |sum| <= 64 * 2^24 (block_finish_row_lean)
-        const int isu = wave_isum((int)((float)util * 0x1p24f));  // (util = 0 where inactive)
-        if (lane == 63) ps[w] = (double)isu;
-      } else {
-        const double su = wave_sum_f64(active ? util : 0.0);
-        if (lane == 63) ps[w] = su;
-      }
-      if (!LEAN) {
-        const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
-        const double sr = wave_sum_f64(srv >= 0 ? rate : 0.0);
-        const double sq = wave_sum_f64(active ? q : 0.0);
-        const double sq2 = wave_sum_f64(active ? q * q : 0.0);
-        const int nlow = __popcll(bal(active && q < kp.qoe_low));
-        if (lane == 63) {
-          ps[16 + w] = sr;
-          ps[32 + w] = sq;
-          ps[48 + w] = sq2;
-          wt[48 + w] = nlow;
+          const double su = wave_sum_f64(active[h] ? util : 0.0);
+          const double q = rint(util * 100.0) / 100.0;  // numpy round(u, 2)
+          const double sr = wave_sum_f64(srv[h] >= 0 ? rate : 0.0);
+          const double sq = wave_sum_f64(active[h] ? q : 0.0);
+          const double sq2 = wave_sum_f64(active[h] ? q * q : 0.0);
+          const int nlow = __popcll(bal(active[h] && q < kp.qoe_low));
+          if (lane == 63) {
+            ps[vw] = su;
+            ps[16 + vw] = sr;
+            ps[32 + vw] = sq;
+            ps[48 + vw] = sq2;
+            wt[48 + vw] = nlow;
+          }
         }
       }
       int ncon = 0;
       if (!LEAN) {
-        const int sc = row_scan_i32(lane < nw ? wt[32 + (lane & 15)] : 0);
-        ncon = __builtin_amdgcn_readlane(sc, nw - 1);
+        const int sc = row_scan_i32(lane < nv ? wt[32 + (lane & 15)] : 0);
+        ncon = __builtin_amdgcn_readlane(sc, nv - 1);
       }
       // the previous step's per-env row (its partial sums are complete: written before this
       // step's barrier)
-      if (LEAN ? (w == 0 && i > 0) : (u == 0 && i > 0)) {
+      if (LEAN ? (w == 0 && i > 0) : (tid == 0 && i > 0)) {
         const double* pps = L.ps + 64 * (par ^ 1);
-        if (LEAN) block_finish_row_lean(kp, out, pps, nw, e, traj ? i - 1 : 0, prev, lane);
-        else block_finish_row<LEAN>(kp, out, pps, L.wt + 64 * (par ^ 1), nw, e, traj ? i - 1 : 0, prev);
+        if (LEAN) block_finish_row_lean(kp, out, pps, nv, e, traj ? i - 1 : 0, prev, lane);
+        else block_finish_row<LEAN>(kp, out, pps, L.wt + 64 * (par ^ 1), nv, e, traj ? i - 1 : 0, prev);
       }
       prev = BlockRow{t + 1, nact, ncon};
       t += 1;
@@ -2793,14 +2890,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       c3 = c3n;
     }
     __syncthreads();  // the last step's partial sums
-    if (LEAN ? (w == 0 && nsteps > 0) : (u == 0 && nsteps > 0)) {
+    if (LEAN ? (w == 0 && nsteps > 0) : (tid == 0 && nsteps > 0)) {
       const int lp = (nsteps - 1) & 1;  // the last step's parity
-      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nw, e, traj ? nsteps - 1 : 0, prev, lane);
-      else block_finish_row<LEAN>(kp, out, L.ps + 64 * lp, L.wt + 64 * lp, nw, e, traj ? nsteps - 1 : 0, prev);
+      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev, lane);
+      else block_finish_row<LEAN>(kp, out, L.ps + 64 * lp, L.wt + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev);
     }
     // ---- epilogue: the state after the last step ----------------------------------------
-    if (valid) store_ue(st.ue_state + idx, pos, wp);
-    if (u == 0) {
+#pragma unroll
+    for (int h = 0; h < UPL; ++h)
+      if (valid[h]) store_ue(st.ue_state + ebase + uh[h], pos[h], wp[h]);
+    if (tid == 0) {
       st.t[e] = t;
       if (M) tb.drawn[e] = drawn;
       if (s_ok || !M) {  // (with a table and drawn <= M its entry is the state: row unchanged)
@@ -3113,6 +3212,7 @@ struct mev_ctx {
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
   int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
+  int upl;            // k_steps_block: UEs per lane (params.ues_per_lane)
   unsigned char* crec_g;  // per-env layouts, block shape: culling records kept in HBM
   uint8_t* crec_ok;       // (mev_update_layouts; KTables::crec_g)
   int het_packed;     // heterogeneous entities on the packed kernels (U <= 64, shared layout;
@@ -3673,6 +3773,9 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     kp.cull_nx = cp.nx;
     kp.cull_nc = cp.nc;
   }
+  // UEs per lane of the block kernel: 1 / 2 forced, 0 per launch (launch_block_steps)
+  c->upl = params->ues_per_lane == 1 || params->ues_per_lane == 2 ? params->ues_per_lane : 0;
+  if (is_het(params)) c->upl = 1;
   {
     const MoveP mp = host_move_params(params->velocity, params->width, params->height);
     kp.vel_f = mp.vel_f;
@@ -4143,10 +4246,23 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                         : (lean ? k_steps_block<false, true, true> : k_steps_block<false, false, true>))
              : (per_env ? (lean ? k_steps_block<true, true, false> : k_steps_block<true, false, false>)
                         : (lean ? k_steps_block<false, true, false> : k_steps_block<false, false, false>));
-  const size_t shm = block_lds_bytes(kp.B, kp.tab_m) + 16 * (size_t)kp.cull_nc;  // (culling records)
+  // two UEs per lane (U > 512, homogeneous) for one-step launches: 1,024 envs of 1,024 UEs then
+  // take 8,192 waves, one round of the chip's resident waves instead of two, and the per-wave
+  // prologue / epilogue is shared by two UEs (custom 128 x 1024 at 1,024 envs: 18.7 -> 17.3 us
+  // per step() launch); rollouts keep one (at full occupancy both shapes issue the same step
+  // work, and the two-UE records need cells twice as wide: 1.41 vs 1.67 ms per 200 steps)
+  const bool one_step = nsteps == 1 || !c->fuse_steps;
+  const int upl = kp.het ? 1 : c->upl > 0 ? c->upl : (kp.U > 512 && one_step ? 2 : 1);
+  if (upl == 2)
+    kf = per_env ? (lean ? k_steps_block<true, true, false, 0, false, 2> : k_steps_block<true, false, false, 0, false, 2>)
+                 : (lean ? k_steps_block<false, true, false, 0, false, 2> : k_steps_block<false, false, false, 0, false, 2>);
+  const CullP cp{kp.cull_log, kp.cull_nx, kp.cull_nc};
+  const size_t shm = block_lds_bytes(kp.B, kp.tab_m) + block_rec_bytes(cp, kp.W, kp.H, nsteps, upl);
   if (lean && per_env && !kp.het && match_scn(c) == 4)  // mobile-custom-128x1024's constants
-    kf = c->tie_free ? k_steps_block<true, true, false, 4, true> : k_steps_block<true, true, false, 4>;
-  const dim3 block((unsigned)((kp.U + 63) / 64 * 64));
+    kf = upl == 2 ? (c->tie_free ? k_steps_block<true, true, false, 4, true, 2> : k_steps_block<true, true, false, 4, false, 2>)
+                  : (c->tie_free ? k_steps_block<true, true, false, 4, true> : k_steps_block<true, true, false, 4>);
+  const int ul = (kp.U + upl - 1) / upl;  // lanes per env
+  const dim3 block((unsigned)((ul + 63) / 64 * 64));
   if (c->fuse_steps || nsteps == 1) {
     launch_k(kf, dim3(kp.E), block, shm, stream, ev, kp, ks, ko, tb, nsteps, traj ? 1 : 0);
   } else {

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -52,6 +52,7 @@ class MevParams(C.Structure):
         ("lds_tables", C.c_int32), ("two_groups", C.c_int32), ("stage_rows", C.c_int32),
         ("xcd_remap", C.c_int32), ("scenario_constants", C.c_int32),
         ("station_culling", C.c_int32),
+        ("ues_per_lane", C.c_int32),
     ]
 
 

@@ -63,6 +63,7 @@ class EngineParams:
     xcd_remap: int = 0           # -1 blocks in dispatch order
     scenario_constants: int = 0  # -1 generic kernel instances only
     station_culling: int = 0     # -1 U > 64: scan every station (no per-cell candidate lists)
+    ues_per_lane: int = 0        # U > 64: 1 / 2 UEs per lane (0: two in one-step launches, U > 512)
     # heterogeneous entities (entities.py:7-22,33-45): parameter classes and each station's /
     # UE's class (None: every entity has bs / ue / velocity above); see lowering.lower
     bs_classes: "list | None" = None   # [{bw, freq, tx, height}]
@@ -144,7 +145,7 @@ class EngineParams:
             lds_tables=int(self.lds_tables), two_groups=int(self.two_groups),
             stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
             scenario_constants=int(self.scenario_constants),
-            station_culling=int(self.station_culling))
+            station_culling=int(self.station_culling), ues_per_lane=int(self.ues_per_lane))
         cp._keep = keep
         return cp
 
