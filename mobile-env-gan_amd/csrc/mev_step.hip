@@ -2467,7 +2467,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const uint64_t lt = (1ull << lane) - 1ull;
   const int M = KPS(tab_m);
   const BlockLds L = block_lds(lds_raw, lds_keys, KPS(B), KPS(tab_m));
-  for (int n = tid; n <= U; n += nt) L.r100[n] = n ? 100.0 / (double)n : 0.0;
+  // 100 / n for n <= rlim: every count for a multi-step launch; a one-step launch fills n <= 64
+  // (one division per lane of the first wave instead of ~two per lane of every wave) and divides
+  // where a station has more (the same correctly rounded value)
+  const int rlim = nsteps == 1 ? min(U, 64) : U;
+  for (int n = tid; n <= rlim; n += nt) L.r100[n] = n ? 100.0 / (double)n : 0.0;
   // station culling: per cell of the map, the stations that can be the closest to some point
   // of the cell (see the prologue)
   const bool CULL = !HET && KPS(cull_log) > 0;
@@ -2830,11 +2834,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         float cents_f = 0.f;
         if (srv[h] >= 0) {
           const int n = cnt[srv[h]];
+          const double r100 = n <= rlim ? L.r100[n] : 100.0 / (double)n;
           if (TF) {  // tie-free table (share_tie_free): the product rounds like the reference
-            cents = rint(full[h] * L.r100[n]);
+            cents = rint(full[h] * r100);
             cents_f = (float)cents;
           } else {
-            cents = share_cents_r(full[h], L.r100[n], n, cents_f);
+            cents = share_cents_r(full[h], r100, n, cents_f);
           }
         }
         const bool exact_util = !LEAN;
