@@ -37,7 +37,8 @@
  *       t       int32 [E]         episode time (base.py:175,280)
  *       bs_xy   int32 [B][2] (shared; the step kernel uses the keys derived from it by
  *                                 mev_reset / mev_update_stations) or [E][B][2] (per env);
- *                                 coordinates in [0, 1024)
+ *                                 coordinates in [0, 1024), or [0, 4096) on a map
+ *                                 beyond 1024 per side
  *       bs_count int32 [E]        per-env number of valid BSs (NULL: all B)
  *     outputs
  *       obs     f32  [E][U][4]    {x/W, y/H, data rate, scaled utility}
@@ -73,7 +74,10 @@ typedef struct mev_params {
   int32_t num_envs;       /* E; E * U < 2^28 per context (shard larger batches) */
   int32_t num_ues;        /* U, 1..1024 */
   int32_t num_bs;         /* B (max per env), 1..1024 */
-  int32_t width, height;  /* map size (base.py:104) */
+  int32_t width, height;  /* map size (base.py:104), 1..4096 per side. Beyond 1024 the
+                             association keys hold the squared distance itself (<= 2 x 1023^2:
+                             a channel that connects farther is refused), per-env layouts with
+                             U <= 64 run on the block kernel, and no LDS tables / culling */
   int32_t ep_max_time;    /* EP_MAX_TIME (base.py:109) */
   int32_t arrival_start;  /* NoDeparture arrival time, 0 (arrival.py:32-33) */
   int32_t arrival_exit;   /* NoDeparture departure time = ep_time (arrival.py:35-36) */

@@ -53,8 +53,13 @@ namespace {
 constexpr int kMaxU = 1024;
 constexpr int kMaxB = 1024;
 constexpr int kMaxClasses = 16;  // station / UE parameter classes (heterogeneous entities)
-// largest squared distance of a UE (inside the map) to a station (coordinates < 1024)
+// largest squared distance of a UE (inside the map) to a station (coordinates < 1024): also
+// the longest connectable distance on the larger maps (kMaxMap), whose association keys hold
+// the squared distance clamped to 22 bits
 constexpr int64_t kD2Top = 2 * 1023 * 1023;
+// map side limit: int16 UE state, and on maps beyond 1024 ("wide") coordinates < 4096, so that a
+// station-to-UE difference fits int16 and its squared length int32
+constexpr int kMaxMap = 4096;
 constexpr int kKeyBits = 10;
 // (d2, bs) association key: BS index in the low kKeyBits bits
 
@@ -2174,10 +2179,25 @@ __global__ __launch_bounds__(1024) void k_reset_block(KParams kp, KState st, KOu
 // Smallest association key over the station pairs [j0, j1) of the LDS key array (two
 // stations per broadcast ds_read_b128): scaled keys dot2(32 p, m) + c, else (dot2(p, m) << 10) + c
 // (see k_steps_block's prologue).
+// (wide maps, W or H > 1024: the keys hold the station itself, {q as int16x2, j}; a UE's key is
+// (min(|p - q|^2, 2^22 - 1) << 10) | j -- the clamp only merges distances far beyond any
+// connectable one, kD2Top < 2^21, whose order does not matter: such a minimum serves nobody)
+__device__ __forceinline__ unsigned wide_key(int2 pos, unsigned qw, unsigned j) {
+  const s16x2 d = s16x2{(short)pos.x, (short)pos.y} - as_s16x2(qw);
+  const unsigned d2 = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
+  return (min(d2, (1u << 22) - 1u) << kKeyBits) | j;
+}
+
 __device__ __forceinline__ unsigned scan_key_pairs(const v4u32* __restrict__ kk2, int j0, int j1,
-                                                   bool scaled, int2 pos) {
+                                                   bool scaled, int2 pos, bool wide = false) {
   unsigned best = UINT_MAX;
-  if (scaled) {
+  if (wide) {
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) {
+      const v4u32 kv = kk2[j];
+      best = min(best, min(wide_key(pos, kv.x, kv.y), wide_key(pos, kv.z, kv.w)));
+    }
+  } else if (scaled) {
     const s16x2 p32 = {(short)(pos.x << 5), (short)(pos.y << 5)};
 #pragma unroll 4
     for (int j = j0; j < j1; ++j) {
@@ -2199,8 +2219,10 @@ __device__ __forceinline__ unsigned scan_key_pairs(const v4u32* __restrict__ kk2
   return best;
 }
 
-// squared distance encoded in an association key of the UE at pos: key - 2^21 + |p|^2
-__device__ __forceinline__ int key_d2(unsigned key, int2 pos) {
+// squared distance encoded in an association key of the UE at pos: key - 2^21 + |p|^2 (wide
+// maps: the key's (clamped) squared distance itself)
+__device__ __forceinline__ int key_d2(unsigned key, int2 pos, bool wide = false) {
+  if (wide) return (int)(key >> kKeyBits);
   return (int)(key >> kKeyBits) - (1 << 21) + (pos.x * pos.x + pos.y * pos.y);
 }
 
@@ -2529,6 +2551,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
     auto tab_at = [&](int k) { return L.tab[k - tb0]; };  // (k < tlim wherever it is read)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
+    const bool wide = KPS(W) > 1024 || KPS(H) > 1024;  // (uniform; a scenario: constant false)
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
     // and stations beyond the env's count get the key that never wins, m = 0, c = UINT_MAX)
     const int nslot = HET ? kp.bperm : nb;
@@ -2539,6 +2562,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         continue;
       }
       const int2 qq = !HET && k == tid ? q_own : bsx[i];
+      if (wide) {  // the station itself (scan_key_pairs' wide form)
+        lds_keys[k] = make_int2((int)(((unsigned)qq.x & 0xffffu) | ((unsigned)qq.y << 16)), i);
+        continue;
+      }
       const int f = scaled ? -64 : -2;
       const s16x2 m2 = {(short)(f * qq.x), (short)(f * qq.y)};
       lds_keys[k] = make_int2(__builtin_bit_cast(int, m2),
@@ -2577,8 +2604,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // the records' cells: the HBM records' (twice as wide) for pers, and in LDS with two UEs per
     // lane (a quarter of the LDS: four workgroups per CU, see block_rec_bytes)
     const CullP pc = pers_cull(CLOG, KPS(W), KPS(H));
-    const bool wide = pers || UPL == 2;
-    const int RLOG = wide ? pc.log : CLOG, RNX = wide ? pc.nx : CNX, RNC = wide ? pc.nc : CNC;
+    const bool wcell = pers || UPL == 2;
+    const int RLOG = wcell ? pc.log : CLOG, RNX = wcell ? pc.nx : CNX, RNC = wcell ? pc.nc : CNC;
     const unsigned char* const grec = pers ? tb.crec_g + (size_t)erec * pc.nc * 16 : nullptr;
     if (cull && !pers) {
       cull_cells(lds_keys, nb, RLOG, RNX, RNC, KPS(W), KPS(H), tid, nt, crec);
@@ -2777,17 +2804,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         int d2s = 0;
         if (!HET) {
           if (active[h] && full_scan[h]) {
-            best[h] = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos[h]);
+            best[h] = scan_key_pairs(kk2, 0, nb >> 1, scaled, pos[h], wide);
             if (nb & 1) {  // the odd last station
               const int2 kv = lds_keys[nb - 1];
               const s16x2 p32 = {(short)(pos[h].x << 5), (short)(pos[h].y << 5)};
               const s16x2 pu = {(short)pos[h].x, (short)pos[h].y};
-              best[h] = min(best[h], scaled ? (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false)
+              best[h] = min(best[h], wide ? wide_key(pos[h], (unsigned)kv.x, (unsigned)kv.y)
+                                     : scaled ? (unsigned)__builtin_amdgcn_sdot2(p32, as_s16x2((unsigned)kv.x), kv.y, false)
                                             : ((unsigned)__builtin_amdgcn_sdot2(pu, as_s16x2((unsigned)kv.x), 0, true) << kKeyBits) +
                                                   (unsigned)kv.y);
             }
           }
-          d2s = key_d2(best[h], pos[h]);
+          d2s = key_d2(best[h], pos[h], wide);
           if (best[h] != UINT_MAX && d2s <= KPS(d2max)) srv[h] = (int)(best[h] & ((1u << kKeyBits) - 1));
           full[h] = tb.rate_full[max(0, min(d2s, KPS(d2max)))];
         } else {
@@ -2796,12 +2824,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           // the smallest key among the connectable class minima (base.py:236-241)
           if (active[h]) {
             for (int c = 0; c < kp.nb_cls; ++c) {
-              const unsigned bc = scan_key_pairs(kk2, tb.seg[c] >> 1, tb.seg[c + 1] >> 1, scaled, pos[h]);
-              if (bc != UINT_MAX && key_d2(bc, pos[h]) <= tb.pair[c * kp.nu_cls + cu].y)
+              const unsigned bc = scan_key_pairs(kk2, tb.seg[c] >> 1, tb.seg[c + 1] >> 1, scaled, pos[h], wide);
+              if (bc != UINT_MAX && key_d2(bc, pos[h], wide) <= tb.pair[c * kp.nu_cls + cu].y)
                 best[h] = min(best[h], bc);
             }
           }
-          d2s = key_d2(best[h], pos[h]);
+          d2s = key_d2(best[h], pos[h], wide);
           if (best[h] != UINT_MAX) {
             srv[h] = (int)(best[h] & ((1u << kKeyBits) - 1));
             full[h] = tb.rate_full[tb.pair[(int)tb.bs_cls[srv[h]] * kp.nu_cls + cu].x + d2s];
@@ -3222,6 +3250,8 @@ struct mev_ctx {
   uint8_t* crec_ok;       // (mev_update_layouts; KTables::crec_g)
   int het_packed;     // heterogeneous entities on the packed kernels (U <= 64, shared layout;
                       // one association map per UE class), else the block kernel
+  int block_small;    // U <= 64 on the block kernel: per-env layouts on a map beyond 1024 (the
+                      // packed kernels' per-env station keys need coordinates < 1024)
   // heterogeneous entities (build_het)
   uint8_t* h_bcl;
   uint8_t* h_ucl;
@@ -3264,7 +3294,7 @@ static int validate(const mev_params* p) {
   if (!p) return MEV_EINVAL;
   if (p->num_envs < 1 || p->num_ues < 1 || p->num_ues > kMaxU) return MEV_EINVAL;
   if (p->num_bs < 1 || p->num_bs > kMaxB) return MEV_EINVAL;
-  if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
+  if (p->width < 1 || p->height < 1 || p->width > kMaxMap || p->height > kMaxMap) return MEV_EINVAL;
   if (p->ep_max_time < 1 || p->arrival_exit < 1) return MEV_EINVAL;
   if (p->stream_split < 0 || p->stream_split > 2) return MEV_EINVAL;
   // every per-UE buffer below 4 GiB (32-bit byte offsets in the step kernel): E U < 2^28
@@ -3576,9 +3606,11 @@ static double host_snr(const mev_params* p, int64_t d2) {
 
 int64_t mev_build_rate_table(const mev_params* p, double* dst, int64_t cap) {
   if (!p || cap < 0 || (cap > 0 && !dst)) return MEV_EINVAL;
-  if (p->width < 1 || p->height < 1 || p->width > 1024 || p->height > 1024) return MEV_EINVAL;
+  if (p->width < 1 || p->height < 1 || p->width > kMaxMap || p->height > kMaxMap) return MEV_EINVAL;
   // connectable d2 = a prefix [0, n): scanned over the map's squared distances, and over every
-  // station distance (coordinates < 1024) when the whole map range connects
+  // station distance (coordinates < 1024) when the whole map range connects; on maps beyond
+  // 1024 the scan stops at kD2Top, and a channel that still connects there is refused (its
+  // keys would not hold the distance)
   const int64_t map_hi = (int64_t)(p->width - 1) * (p->width - 1) +
                          (int64_t)(p->height - 1) * (p->height - 1);
   int64_t n = 0;
@@ -3592,6 +3624,7 @@ int64_t mev_build_rate_table(const mev_params* p, double* dst, int64_t cap) {
       n = d2 + 1;
     }
   }
+  if (map_hi > kD2Top && n == kD2Top + 1) return MEV_EINVAL;
   return prefix ? n : MEV_ECHANNEL;
 }
 
@@ -3724,6 +3757,11 @@ static KTables tables_of(const mev_ctx* c) {
   tb.crec_g = c->crec_g;
   tb.crec_ok = c->crec_ok;
   return tb;
+}
+
+// The packed step shape (several envs per wavefront), else the block shape (a workgroup per env).
+static bool packed_shape(const mev_ctx* c) {
+  return c->kp.U <= 64 && (!c->kp.het || c->het_packed) && !c->block_small;
 }
 
 // The body of mev_create on a value-initialised context; on any failure the caller releases
@@ -3862,9 +3900,12 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   //      <= 1024 x 1024 x 16 B)
   c->assoc = nullptr;
   c->het_packed = c->kp.het && params->num_ues <= 64 && !params->bs_per_env;
+  c->block_small = params->num_ues <= 64 && params->bs_per_env &&
+                   (params->width > 1024 || params->height > 1024);
   if (!params->bs_per_env && (!c->kp.het || c->het_packed)) {
     const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height *
                          (size_t)(c->het_packed ? c->kp.nu_cls : 1);
+    if (bytes >= ((size_t)1 << 32)) return MEV_EINVAL;  // (32-bit byte offsets in the gather)
     if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
       return MEV_ENOMEM;
     }
@@ -3920,7 +3961,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   //      two streams (measured 3-5 % faster at 65536 large envs, but the overlapping
   //      dispatches cannot be timed one by one)
   c->parts = 1;
-  if (c->kp.U <= 64 && params->stream_split == 2) c->parts = 2;
+  if (c->kp.U <= 64 && !c->block_small && params->stream_split == 2) c->parts = 2;
   c->fuse_steps = params->fuse_steps >= 0;
   if (c->parts == 2) {
     MEV_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
@@ -3977,7 +4018,7 @@ int mev_launch_parts(const mev_ctx* c) { return c ? c->parts : MEV_EINVAL; }
 
 int mev_step_shape(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
-  return c->kp.U <= 64 && (!c->kp.het || c->het_packed) ? 1 : 2;
+  return packed_shape(c) ? 1 : 2;
 }
 
 int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EINVAL; }
@@ -4289,7 +4330,7 @@ static int launch(const mev_ctx* c, const mev_state* st, const mev_outputs* out,
   to_kernel(st, out, ks, ko);
   const KTables tb = tables_of(c);
   const KParams& kp = c->kp;
-  if (kp.U <= 64 && (!kp.het || c->het_packed)) {
+  if (packed_shape(c)) {
     const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
     if (RESET) {
       const dim3 grid((unsigned)((groups + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -4423,7 +4464,7 @@ static int run_steps(const mev_ctx* c, const mev_state* st, const mev_outputs* o
     if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, (hipStream_t)stream));
     return MEV_OK;
   }
-  if (c->kp.U <= 64 && (!c->kp.het || c->het_packed))
+  if (packed_shape(c))
     return launch_packed_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
   return launch_block_steps(c, ks, ko, tb, nsteps, traj, (hipStream_t)stream, ev);
 }

@@ -22,7 +22,9 @@ import math
 import numpy as np
 
 EPSILON = 1e-16  # channels.py:8
-# largest squared distance of a UE on the map to a station (coordinates < 1024, mev.h)
+# largest squared distance of a UE on the map to a station (coordinates < 1024, mev.h); on maps
+# beyond 1024 also the longest connectable distance (mev.h kMaxMap: the association keys hold
+# the squared distance in 22 bits)
 D2_TOP = 2 * 1023 * 1023
 
 
@@ -71,8 +73,11 @@ class Channel:
 
     def _rate_table(self, bs: dict, ue: dict, width: int, height: int):
         map_hi = (width - 1) ** 2 + (height - 1) ** 2
-        snr = self._snr_table(map_hi, bs, ue)
+        snr = self._snr_table(min(map_hi, D2_TOP), bs, ue)
         conn = snr > ue["snr_tr"]
+        if conn.all() and map_hi > D2_TOP:  # (maps beyond 1024: as mev_build_rate_table)
+            raise ValueError("the channel connects beyond the longest supported distance "
+                             f"(d2 > {D2_TOP}) on a {width} x {height} map")
         if conn.all():  # every map distance connects: stations may sit off the map
             snr = self._snr_table(D2_TOP, bs, ue)
             conn = snr > ue["snr_tr"]

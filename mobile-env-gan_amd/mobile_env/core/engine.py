@@ -176,15 +176,22 @@ class Trajectory:
                           v(self.rate64), v(self.util64), v(self.metrics))
 
 
-def _check_station_range(bs, bs_count=None):
-    """Station coordinates must lie in [0, 1024) (mev.h: the association keys are 32-bit);
-    per-env layouts with a station count: only the first bs_count[e] rows are stations."""
+def station_limit(width: int, height: int) -> int:
+    """Station coordinates lie in [0, limit): 1024 on maps up to 1024 x 1024 (the association
+    keys hold |p - q|^2 - |p|^2 in 32 bits), 4096 on larger maps (mev.h kMaxMap: the keys hold
+    the clamped squared distance itself)."""
+    return 1024 if width <= 1024 and height <= 1024 else 4096
+
+
+def _check_station_range(bs, bs_count=None, limit: int = 1024):
+    """Station coordinates must lie in [0, limit) (station_limit); per-env layouts with a
+    station count: only the first bs_count[e] rows are stations."""
     if bs_count is not None and bs.dim() == 3:
         cnt = torch.as_tensor(bs_count, dtype=torch.int64, device=bs.device).reshape(-1, 1)
         keep = torch.arange(bs.shape[1], device=bs.device)[None, :] < cnt
         bs = bs[keep]
-    if bs.numel() and (int(bs.min()) < 0 or int(bs.max()) > 1023):
-        raise ValueError("base-station coordinates must lie in [0, 1024)")
+    if bs.numel() and (int(bs.min()) < 0 or int(bs.max()) > limit - 1):
+        raise ValueError(f"base-station coordinates must lie in [0, {limit})")
 
 
 def _ptr(t):
@@ -218,7 +225,7 @@ class StepEngine:
         B = bs.shape[-2]
         if B != params.num_bs:
             raise ValueError(f"bs_xy has {B} stations, params say {params.num_bs}")
-        _check_station_range(bs, bs_count)
+        _check_station_range(bs, bs_count, station_limit(params.width, params.height))
         L = N.lib()
         with torch.cuda.device(device):
             tab = params.rate_table()  # the reference's own values (numpy, host)
@@ -366,7 +373,7 @@ class StepEngine:
         bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)
         if tuple(bs.shape) != tuple(self.bs_xy.shape):
             raise ValueError("layout shape mismatch")
-        _check_station_range(bs, bs_count)
+        _check_station_range(bs, bs_count, station_limit(self.p.width, self.p.height))
         if bs_count is not None and self.bs_count is None:
             raise ValueError("engine was built without bs_count")
         self.bs_xy.copy_(bs)

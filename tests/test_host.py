@@ -81,7 +81,7 @@ def test_create_rejects_bad_params_without_gpu():
     from mobile_env.core.engine import EngineParams
     lib = N.lib()
     for bad in (dict(num_envs=0), dict(num_ues=0), dict(num_ues=1025), dict(num_bs=0),
-                dict(width=2000), dict(stream_split=3)):
+                dict(width=4097), dict(height=5000), dict(stream_split=3)):
         kw = dict(num_envs=4, num_ues=5, num_bs=3)
         kw.update(bad)
         cp = EngineParams(**kw).to_c(False)
@@ -200,6 +200,39 @@ def test_station_range_check():
     _check_station_range(lay, [1, 2])
     with pytest.raises(ValueError):
         _check_station_range(lay, [2, 2])
+    # maps beyond 1024 (mev.h kMaxMap): stations anywhere in [0, 4096)
+    from mobile_env.core.engine import station_limit
+    assert station_limit(200, 1024) == 1024 and station_limit(1025, 30) == 4096
+    _check_station_range(torch.tensor([[0, 0], [4095, 5]]), limit=station_limit(3000, 2000))
+    with pytest.raises(ValueError):
+        _check_station_range(torch.tensor([[4096, 0]]), limit=4096)
+
+
+def test_wide_map_rate_tables():
+    """Maps beyond 1024 x 1024: the Python (numpy) and C (libm) tables scan the squared
+    distances up to D2_TOP and agree on the connectable range; a channel that still connects
+    at D2_TOP is refused by both (the association keys hold the squared distance in 22 bits)."""
+    import ctypes as C
+    from mobile_env.core import _native as N
+    from mobile_env.core.channels import D2_TOP, OkumuraHata
+    from mobile_env.core.engine import EngineParams
+    lib = N.lib()
+    bs = {"bw": 9e6, "freq": 2500, "tx": 55, "height": 50}
+    ue = {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
+    tab = OkumuraHata().rate_table(bs, ue, 3000, 2000)
+    cp = EngineParams(num_envs=1, num_ues=5, num_bs=3, width=3000, height=2000, bs=bs,
+                      ue=ue).to_c(False)
+    n = lib.mev_build_rate_table(C.byref(cp), None, 0)
+    assert n == len(tab) and 19363 < n < D2_TOP
+    ctab = np.zeros(n)
+    assert lib.mev_build_rate_table(C.byref(cp), ctab.ctypes.data, n) == n
+    np.testing.assert_allclose(ctab, tab, rtol=1e-13, atol=0)  # (libm vs numpy's log10 / pow)
+    strong = dict(bs, tx=90)
+    with pytest.raises(ValueError):
+        OkumuraHata().rate_table(strong, ue, 3000, 2000)
+    cp = EngineParams(num_envs=1, num_ues=5, num_bs=3, width=3000, height=2000, bs=strong,
+                      ue=ue).to_c(False)
+    assert lib.mev_build_rate_table(C.byref(cp), None, 0) == N.MEV_EINVAL
 
 
 def test_bench_byte_models():
