@@ -2547,25 +2547,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // U initial positions, then the draws) or from `drawn` (the draws: at most U)
     const int tb0 = nsteps == 1 ? (t >= KPS(t_end) ? 0 : drawn) : 0;
     const int tlim = nsteps == 1 ? min(M, tb0 + 2 * U) : M;
-    // (the first 8 rows of the copy with every load issued before the first LDS store -- the
-    // plain loop waited for each load before its store, a chain of up to seven global round
-    // trips per wave in a one-step launch -- then the rest of a long table, if any)
-    if (M) {
-      constexpr int TQ = 8;
-      const int* const src = tb.tab_xy + (size_t)e * M;
-      int tv[TQ];
-#pragma unroll
-      for (int q = 0; q < TQ; ++q) {
-        const int k = tb0 + tid + q * nt;
-        tv[q] = k < tlim ? src[k] : 0;
-      }
-#pragma unroll
-      for (int q = 0; q < TQ; ++q) {
-        const int k = tb0 + tid + q * nt;
-        if (k < tlim) L.tab[k - tb0] = tv[q];
-      }
-      for (int k = tb0 + tid + TQ * nt; k < tlim; k += nt) L.tab[k - tb0] = src[k];
-    }
+    if (M)
+      for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
     auto tab_at = [&](int k) { return L.tab[k - tb0]; };  // (k < tlim wherever it is read)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     const bool wide = KPS(W) > 1024 || KPS(H) > 1024;  // (uniform; a scenario: constant false)
