@@ -2735,7 +2735,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 #pragma unroll
       for (int h = 0; h < UPL; ++h)
         if (active[h]) move_ue_p(pos[h], wp[h], mp);
-      ahead_counts(t + 1, wp, L.wt + 64 * (par ^ 1));  // the next step's, after this move
+      // the next step's, after this move (none after a launch's last step: the next launch's
+      // prologue counts from the stored state)
+      if (i + 1 < nsteps) ahead_counts(t + 1, wp, L.wt + 64 * (par ^ 1));
 
       // ---- association: min over the env's station keys (LDS broadcast reads) ----------
       // (ext_vector_type loads: one broadcast ds_read_b128 per two stations; HIP's int4 struct is
