@@ -2545,11 +2545,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // the episode draw table in LDS: all M pairs for launches of several steps; a one-step
     // launch copies only the window it can use, 2U pairs from `tb` = 0 (a reset this step: the
     // U initial positions, then the draws) or from `drawn` (the draws: at most U)
-    const int tb0 = nsteps == 1 ? (t >= KPS(t_end) ? 0 : drawn) : 0;
-    const int tlim = nsteps == 1 ? min(M, tb0 + 2 * U) : M;
-    if (M)
-      for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tb.tab_xy[(size_t)e * M + k];
-    auto tab_at = [&](int k) { return L.tab[k - tb0]; };  // (k < tlim wherever it is read)
+    // (a one-step launch reads its few pairs straight from HBM instead: the copy loop waits for
+    // each of a lane's loads before its store, a chain of global round trips in the prologue)
+    const bool tab_g = nsteps == 1;
+    const int* const tab_src = tb.tab_xy + (size_t)e * M;
+    const int tb0 = 0;
+    const int tlim = M;
+    if (M && !tab_g)
+      for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tab_src[k];
+    auto tab_at = [&](int k) { return tab_g ? tab_src[k] : L.tab[k - tb0]; };  // (k < M)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     const bool wide = KPS(W) > 1024 || KPS(H) > 1024;  // (uniform; a scenario: constant false)
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
