@@ -20,11 +20,16 @@ Contract (see DESIGN.md "Measurement"):
 * Warmup: W steps, and then more until ``--warmup-floor-s`` seconds of back-to-back launches
   have run (untimed; the chip reaches its steady clock -- a 5-step warmup would time a cold
   launch). ``warmup`` in the line is W as requested; ``warmup_executed`` what ran.
-* Timed region: barrier + synchronize, the K steps, the single final all-gather of the
-  (reward, done) batch over RCCL when N > 1, synchronize + barrier. value = N*E*K / max-over-
-  ranks time. Inputs are resident in HBM before timing starts.
+* Timed region: barrier + synchronize, the K steps, and when N > 1 a synchronize and the single
+  final all-gather of the (reward, done) batch over RCCL, synchronize + barrier. value = N*E*K /
+  max-over-ranks time. Nothing else runs inside it (no event record). Inputs are resident in
+  HBM before timing starts. With N > 1 both collectives (final batch, obs) run once in the
+  untimed warmup, so the timed gather is not the process's first; the line reports the timed
+  gather's own wall time (`distributed.final_gather_ms`, its share of the window) and the
+  rate without it (`distributed.value_steps_only`).
 * roofline (the timed launch shape): algorithmic bytes per launch over the launch's average
-  duration from HIP events on the stream the kernel runs on. A rollout launch of n steps keeps
+  duration from HIP events on the stream the kernel runs on, measured after the timed region
+  on 30 launches of the timed shape (isolated launches when the region was one launch). A rollout launch of n steps keeps
   the env state in registers between its steps, so its algorithmic bytes are every step's
   outputs, E * n * (20*U + 5), plus the canonical state read and written once,
   E * (34*U + 56); SURVEY.md 8d's canonical per-step figure (54*U + 61 B per env-step) counts a
@@ -88,21 +93,48 @@ def chunk_plan(steps: int, chunk: int):
     return plan
 
 
-def timed_run(issue, plan, sync, barrier, make_event, collective):
-    """The timed region: barrier + sync, every launch of `plan` with an event pair around it,
-    the final collective, sync + barrier. Returns (wall seconds, [(start, end, n)])."""
-    events = [(make_event(), make_event(), n) for n in plan]
+def timed_run(issue, plan, sync, barrier, collective=None):
+    """The timed region: barrier + sync, every launch of `plan`, the final collective (if any),
+    sync + barrier. Nothing else happens inside it: no event is recorded (a launch's duration
+    is measured after the region, `launch_timing`). With a collective the launches are
+    synchronised before it, so that its share of the window is known (`final_gather_ms`).
+    Returns (wall s of the region, wall s to the end of the launches, wall s of the collective)."""
     barrier()
     sync()
     t0 = time.perf_counter()
-    for a, b, n in events:
+    for n in plan:
+        issue(n)
+    t_steps = t_coll = None
+    if collective is not None:
+        sync()
+        t_steps = time.perf_counter() - t0
+        collective()
+    sync()
+    t_end = time.perf_counter()
+    if collective is not None:
+        t_coll = t_end - t0 - t_steps
+    else:
+        t_steps = t_end - t0
+    barrier()
+    return time.perf_counter() - t0, t_steps, t_coll
+
+
+def launch_timing(issue, n, reps, sync, make_event, isolated):
+    """Average duration in ms of a launch of n steps, from an event pair around each of `reps`
+    launches on the launch stream, run AFTER the timed region: isolated launches (synchronize
+    before each; the shape of a timed region of one launch, the driver's --steps 20) or back to
+    back (the shape of a timed region of many launches). Returns (mean, median) in ms."""
+    evs = [(make_event(), make_event()) for _ in range(reps)]
+    sync()
+    for a, b in evs:
+        if isolated:
+            sync()
         a.record()
         issue(n)
         b.record()
-    collective()
     sync()
-    barrier()
-    return time.perf_counter() - t0, events
+    ms = sorted(a.e.elapsed_time(b.e) for a, b in evs)
+    return sum(ms) / len(ms), ms[len(ms) // 2]
 
 
 def max_over_ranks(value: float, device=None) -> float:
@@ -392,12 +424,14 @@ def main():
 
     gathered = {}
 
-    def collective():
-        if world > 1:  # the one collective: final (reward, done) batch to every rank
-            if traj is not None:  # the last step's row of the trajectory
-                gathered["rd"] = gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
-            else:
-                gathered["rd"] = gather_final(eng.reward, eng.done)
+    def collective():  # the one collective: the final (reward, done) batch to every rank
+        if traj is not None:  # the last step's row of the trajectory
+            gathered["rd"] = gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
+        else:
+            gathered["rd"] = gather_final(eng.reward, eng.done)
+
+    def obs_last():
+        return traj.obs[plan[-1] - 1] if traj is not None else eng.obs
 
     # warmup: W steps, then whole chunks until the floor time has passed (steady clock)
     warm = 0
@@ -415,34 +449,50 @@ def main():
                 warm += CHUNK
             sync()
     sync()
+    warm_gathers = None
+    if world > 1:  # both collectives once, untimed: the timed one is not the process's first
+        t0 = time.perf_counter()
+        collective()
+        sync()
+        t1 = time.perf_counter()
+        gather_obs(obs_last())
+        sync()
+        warm_gathers = {"final_ms": (t1 - t0) * 1e3, "obs_ms": (time.perf_counter() - t1) * 1e3}
+        gathered.clear()
 
     for n in set(plan):  # every launch of the timed region prebuilt
         if n not in launchers:
             launchers[n] = eng.launcher(n, traj)
     barrier = dist.barrier if world > 1 else (lambda: None)
-    elapsed, events = timed_run(issue, plan, sync, barrier, _WallEv if stub else _Ev, collective)
+    elapsed, t_steps, t_gather = timed_run(issue, plan, sync, barrier,
+                                           collective if world > 1 else None)
     elapsed = max_over_ranks(elapsed, device)
+    t_steps = max_over_ranks(t_steps, device)
+    t_gather = max_over_ranks(t_gather, device) if t_gather is not None else None
 
     # after the timed region: the north-star final obs batch to every rank (RCCL all-gather over
     # xGMI; obs of the last step), timed on its own (barrier + sync around, max over ranks)
     obs_gather = None
     if world > 1:
-        obs_last = traj.obs[plan[-1] - 1] if traj is not None else eng.obs
+        ol = obs_last()
         barrier()
         sync()
         t0 = time.perf_counter()
-        g_obs = gather_obs(obs_last)
+        g_obs = gather_obs(ol)
         sync()
         ms = max_over_ranks((time.perf_counter() - t0) * 1e3, device)
-        nbytes = obs_last.numel() * obs_last.element_size()
+        nbytes = ol.numel() * ol.element_size()
         obs_gather = {"ms": ms, "bytes_per_rank": nbytes, "gathered_bytes": world * nbytes,
                       "shape": list(g_obs.shape), "backend": dist.get_backend(),
                       "bus_GBps": (world - 1) * nbytes / (ms * 1e-3) / 1e9,
                       "checksum": float(g_obs[..., 0].double().sum())}
         del g_obs
-    # the launch shape's average duration over the full-size launches (events on the stream)
-    full = [a.e.elapsed_time(b.e) for a, b, n in events if n == CHUNK]
-    chunk_ms = sum(full) / len(full)
+    # the launch shape's duration, measured after the timed region with an event pair around
+    # each launch: isolated launches when the region was one launch (the driver's shape), else
+    # back to back like the region's
+    reps = max(3, min(30, int(0.05 / max(CHUNK * 8e-6, 1e-6))))
+    chunk_ms, chunk_ms_med = launch_timing(issue, CHUNK, reps, sync, _WallEv if stub else _Ev,
+                                           isolated=len(plan) == 1)
 
     step_roof = None
     if rank == 0 and fused and not args.profile_run and args.step_launches > 0 and not stub:
@@ -491,6 +541,9 @@ def main():
             "canonical_equiv_achieved": canon_bytes / (launch_ms * 1e-3) / 1e9,
             "canonical_equiv_frac": canon_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "steps_per_launch": spl,
+            "launch_ms_median": chunk_ms_med if fused else chunk_ms_med / CHUNK,
+            "launch_ms_basis": (f"HIP events around {reps} {'isolated' if len(plan) == 1 else 'back-to-back'} "
+                                f"launches of the timed shape, run after the timed region"),
             "rocprof_launch_ms": rocprof_ms,
             "launch_shape": (
                 f"fused rollout: {spl} steps per launch, env state in registers between "
@@ -520,6 +573,10 @@ def main():
             "cpu_baseline": cpu,
             "distributed": ({"world_size_seen": dist.get_world_size(),
                              "backend": dist.get_backend(),
+                             "final_gather_ms": t_gather * 1e3,
+                             "final_gather_share": t_gather / elapsed,
+                             "value_steps_only": world * E * K / t_steps,
+                             "warmup_gathers": warm_gathers,
                              "final_batch": {"shape": list(gathered["rd"].shape),
                                              "reward_sum": float(gathered["rd"][:, 0].double().sum()),
                                              "done_sum": float(gathered["rd"][:, 1].double().sum())},

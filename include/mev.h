@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 18
+#define MEV_ABI_VERSION 19
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -259,6 +259,17 @@ int mev_prepare_draws(const mev_ctx* ctx, const mev_state* state, const uint8_t*
  * movement.py:44-47,64-72) into its pcg row: the step kernels skip that write while an
  * episode's draws stay inside the episode draw table (mev_state.pcg). Stream-ordered. */
 int mev_sync_stream_state(const mev_ctx* ctx, const mev_state* st, void* stream);
+
+/* Restore a checkpoint mid-episode: after writing saved {ue_state, pcg, t} rows (pcg saved
+ * after mev_sync_stream_state) into this context's state buffers, declare that the pcg rows of
+ * the envs with env_mask[e] (all if NULL) hold their CURRENT stream states. Their waypoint
+ * draws (movement.py:44-47) then continue from those rows -- not from the episode draw table,
+ * whose position in the episode this context does not know -- until each env's next reset,
+ * which returns it to the table (rebuilt here from the rows' state0, as mev_prepare_draws).
+ * Without it a restored env would re-read the episode's first table pairs. No-op without a draw
+ * table. Stream-ordered. */
+int mev_restore_stream_state(const mev_ctx* ctx, const mev_state* st, const uint8_t* env_mask,
+                             void* stream);
 
 /* Shared station layout (bs_per_env = 0): (re)derive the association keys the step kernel
  * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the

@@ -703,6 +703,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uin
 // state between a > 8-byte buffer store and a VALU write of its data registers, and on gfx950
 // that write then corrupts the stored data (seen as other values in a few obs rows;
 // tools/check_store_hazard.py checks the generated assembly for such stores).
+// Cache policy of the per-UE trajectory stores (dev A/B knob: 0 default, 2 nt, 16 sc1)
+#ifndef MEV_TRAJ_AUX
+#define MEV_TRAJ_AUX 0
+#endif
 template <bool LEAN, bool SMALL = true>
 __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p, uint32_t E,
                                               uint32_t EU, uint32_t row) {
@@ -711,9 +715,9 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
                     __float_as_uint(p.obs.z), __float_as_uint(p.obs.w)};
   const size_t ru = (size_t)row * EU, re = (size_t)row * E;
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)p.srv, out_rsrc(out.serving + ru, rsrv),
-                                        p.valid ? 4u * p.ui : rsrv, 0, 0);
+                                        p.valid ? 4u * p.ui : rsrv, 0, MEV_TRAJ_AUX);
   __builtin_amdgcn_raw_buffer_store_b128(ob, out_rsrc(out.obs + ru, robs),
-                                         p.valid ? 16u * p.ui : robs, 0, 0);
+                                         p.valid ? 16u * p.ui : robs, 0, MEV_TRAJ_AUX);
   if (SMALL) {  // (else staged in LDS by the caller: k_steps_packed, STG)
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p.reward), out_rsrc(out.reward + re, rrew),
                                           p.lead ? 4u * (uint32_t)p.e : rrew, 0, 0);
@@ -3197,6 +3201,16 @@ __global__ void k_sync_stream_state(int E, int M, const int* __restrict__ drawn,
   *reinterpret_cast<ulonglong2*>(pcg + (size_t)6 * e) = make_ulonglong2((uint64_t)s, (uint64_t)(s >> 64));
 }
 
+// A checkpoint restored into this context (mev_restore_stream_state): the pcg rows of the envs
+// with mask[e] hold their current stream states, so their draws come from the row, not from
+// the episode draw table, until their next reset (drawn > M: the kernels' stream-state path).
+__global__ void k_restore_stream_state(int E, int M, const uint8_t* __restrict__ mask,
+                                       int* __restrict__ drawn) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E || (mask && !mask[e])) return;
+  drawn[e] = M + 1;
+}
+
 // Jump table for k in [0, kmax]: a^k and G(k) = 1 + a + ... + a^(k-1) (mod 2^128).
 __global__ void k_jump_table(int kmax, u128* __restrict__ jump) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3902,15 +3916,19 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
                      c->jump);
   MEV_HIP(hipGetLastError());
 
-  // ---- association map of a shared layout (filled by mev_reset / mev_update_stations;
-  //      <= 1024 x 1024 x 16 B)
+  // ---- association map of a shared layout (filled by mev_reset / mev_update_stations), only
+  //      for the packed kernels (U <= 64) that gather from it: W x H x 16 B per map (268 MB at
+  //      4,096^2), one per UE class with heterogeneous entities. Heterogeneous maps of 4 GiB or
+  //      more (32-bit byte offsets in the gather) leave the context on the block kernel, which
+  //      scans the stations instead.
   c->assoc = nullptr;
-  c->het_packed = c->kp.het && params->num_ues <= 64 && !params->bs_per_env;
+  const size_t map1 = sizeof(int4) * (size_t)params->width * (size_t)params->height;
+  c->het_packed = c->kp.het && params->num_ues <= 64 && !params->bs_per_env &&
+                  map1 * (size_t)c->kp.nu_cls < ((size_t)1 << 32);
   c->block_small = params->num_ues <= 64 && params->bs_per_env &&
                    (params->width > 1024 || params->height > 1024);
-  if (!params->bs_per_env && (!c->kp.het || c->het_packed)) {
-    const size_t bytes = sizeof(int4) * (size_t)params->width * (size_t)params->height *
-                         (size_t)(c->het_packed ? c->kp.nu_cls : 1);
+  if (!params->bs_per_env && params->num_ues <= 64 && (!c->kp.het || c->het_packed)) {
+    const size_t bytes = map1 * (size_t)(c->het_packed ? c->kp.nu_cls : 1);
     if (bytes >= ((size_t)1 << 32)) return MEV_EINVAL;  // (32-bit byte offsets in the gather)
     if (hipMalloc(&c->assoc, bytes) != hipSuccess) {
       return MEV_ENOMEM;
@@ -4366,6 +4384,7 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        nullptr, 0, c->crec_g, c->crec_ok);
     MEV_HIP(hipGetLastError());
   }
+  if (!c->assoc) return MEV_OK;  // (block shape: no association map, no LDS tables)
   const int cells = c->p.width * c->p.height;
   if (c->het_packed) {  // one map per UE class
     const int n = cells * c->kp.nu_cls;
@@ -4439,6 +4458,19 @@ int mev_sync_stream_state(const mev_ctx* c, const mev_state* st, void* stream) {
   if (!c->kp.tab_m) return MEV_OK;  // without the table the rows are always current
   hipLaunchKernelGGL(k_sync_stream_state, dim3((unsigned)((c->kp.E + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, c->kp.E, c->kp.tab_m, c->drawn, c->tab_st, st->pcg);
+  MEV_HIP(hipGetLastError());
+  return MEV_OK;
+}
+
+int mev_restore_stream_state(const mev_ctx* c, const mev_state* st, const uint8_t* env_mask,
+                             void* stream) {
+  if (!c || !st || !st->pcg) return MEV_EINVAL;
+  if (!c->kp.tab_m) return MEV_OK;  // without the table every draw reads the row already
+  // the episode draw tables of the restored streams (state0), for the envs' next episodes
+  const int rc = mev_prepare_draws(c, st, env_mask, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_restore_stream_state, dim3((unsigned)((c->kp.E + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, c->kp.E, c->kp.tab_m, env_mask, c->drawn);
   MEV_HIP(hipGetLastError());
   return MEV_OK;
 }

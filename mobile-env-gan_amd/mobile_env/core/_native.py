@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -26,7 +26,7 @@ EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_lau
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations", "mev_update_layouts", "mev_build_rate_table", "mev_share_cents",
            "mev_rollout_instance", "mev_share_tie_free",
-           "mev_reset", "mev_prepare_draws", "mev_sync_stream_state", "mev_step", "mev_rollout", "mev_rollout_timed", "mev_strerror", "mev_last_hip_error")
+           "mev_reset", "mev_prepare_draws", "mev_sync_stream_state", "mev_restore_stream_state", "mev_step", "mev_rollout", "mev_rollout_timed", "mev_strerror", "mev_last_hip_error")
 
 
 class MevParams(C.Structure):
@@ -116,6 +116,9 @@ def lib():
         L.mev_prepare_draws.restype = C.c_int
         L.mev_sync_stream_state.argtypes = [C.c_void_p, C.POINTER(MevState), C.c_void_p]
         L.mev_sync_stream_state.restype = C.c_int
+        L.mev_restore_stream_state.argtypes = [C.c_void_p, C.POINTER(MevState), C.c_void_p,
+                                               C.c_void_p]
+        L.mev_restore_stream_state.restype = C.c_int
         L.mev_update_stations.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mev_update_stations.restype = C.c_int
         L.mev_update_layouts.argtypes = [C.c_void_p, C.POINTER(MevState), C.c_void_p, C.c_void_p]

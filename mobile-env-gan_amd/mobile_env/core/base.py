@@ -144,8 +144,7 @@ class MComCore:
             return self._engine
         carry = None
         if self._engine is not None:  # new layout (MComCustom): keep the movement stream
-            self._engine.sync_stream_state()
-            carry = (self._engine.pcg.clone(), self._engine.t.clone())
+            carry = (self._engine.pcg.clone(), self._engine.t.clone())  # (pcg: synced)
             self._engine.close()
         p = lowering.lower(num_envs=1, stations=stations, users=users,
                            arrival=self.arrivalModel, channel=self.channelModel,
@@ -158,7 +157,7 @@ class MComCore:
         self._engine = StepEngine(p, bs_xy, [self.movementModel.seed - 4], device=self.device,
                                   rate64=True, util64=True, metrics=True)
         if carry is not None:
-            self._engine.pcg.copy_(carry[0])
+            self._engine._pcg.copy_(carry[0])
             self._engine.t.copy_(carry[1])
         self._engine_key = key
         return self._engine

@@ -244,7 +244,7 @@ class StepEngine:
                     raise ValueError("bs_count out of range")
             self.ue_state = torch.full((E, U, 4), -1, dtype=torch.int16, **kw)
             self.t = torch.full((E,), params.t_end, dtype=torch.int32, **kw)
-            self.pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
+            self._pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
             self.obs = torch.zeros((E, U, 4), dtype=torch.float32, **kw)
             self.serving = torch.full((E, U), -1, dtype=torch.int32, **kw)
             self.reward = torch.zeros((E,), dtype=torch.float32, **kw)
@@ -264,7 +264,7 @@ class StepEngine:
 
     # -- plumbing -----------------------------------------------------------------------------
     def _bind(self):
-        self._st = N.MevState(_ptr(self.ue_state), _ptr(self.pcg), _ptr(self.t),
+        self._st = N.MevState(_ptr(self.ue_state), _ptr(self._pcg), _ptr(self.t),
                               _ptr(self.bs_xy), _ptr(self.bs_count))
         self._out = N.MevOutputs(_ptr(self.obs), _ptr(self.serving), _ptr(self.reward),
                                  _ptr(self.done), _ptr(self.rate64), _ptr(self.util64),
@@ -350,24 +350,56 @@ class StepEngine:
         if len(s) >= 4096:  # SeedSequence hashing on the device for large batches
             d_seeds = torch.from_numpy(s + 4).to(self.device)
             with torch.cuda.device(self.device):
-                N.check(self._lib.mev_seed_pcg64_device(_ptr(d_seeds), len(s), _ptr(self.pcg),
+                N.check(self._lib.mev_seed_pcg64_device(_ptr(d_seeds), len(s), _ptr(self._pcg),
                                                         self._stream()),
                         "mev_seed_pcg64_device")
         else:
             rows = N.seed_pcg64((s + 4).astype(np.uint64))
-            self.pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
+            self._pcg.copy_(torch.from_numpy(rows.view(np.int64)).to(self.device))
         self.t.fill_(self.p.t_end)
         with torch.cuda.device(self.device):  # the episode draw tables follow the new streams
             N.check(self._lib.mev_prepare_draws(self._ctx, C.byref(self._st), None,
                                                 self._stream()), "mev_prepare_draws")
 
     def sync_stream_state(self):
-        """Materialise every env's movement stream state in ``pcg`` (mev_sync_stream_state):
+        """Materialise every env's movement stream state in the pcg rows (mev_sync_stream_state):
         with the episode draw table the kernels leave the state column as it is while an
-        episode's draws stay inside the table. Call before reading or saving ``pcg``."""
+        episode's draws stay inside the table. (``pcg`` does this on every read.)"""
         with torch.cuda.device(self.device):
             N.check(self._lib.mev_sync_stream_state(self._ctx, C.byref(self._st), self._stream()),
                     "mev_sync_stream_state")
+
+    @property
+    def pcg(self):
+        """The movement streams [E, 6] int64 {state, inc, state0} (u128 each, numpy PCG64,
+        movement.py:16-18), every state current: reading it synchronises the state column first
+        (mev_sync_stream_state), so a saved copy is a valid checkpoint. Writes to the returned
+        tensor reach the engine's rows; after writing mid-episode states call
+        ``restore_state`` (or use it to write them)."""
+        self.sync_stream_state()
+        return self._pcg
+
+    def restore_state(self, ue_state, pcg, t, mask=None):
+        """Load a checkpoint {ue_state [E,U,4] int16, pcg [E,6] (as read from ``pcg``), t [E]}
+        taken at any step of an episode (all envs, or those with mask[e]) and continue from it:
+        the envs' waypoint draws continue from the saved stream states until their next reset
+        (mev_restore_stream_state), exactly as the saving engine would have continued."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.bool)
+        src = [torch.as_tensor(x, device=self.device) for x in (ue_state, pcg, t)]
+        for dst, x in zip((self.ue_state, self._pcg, self.t), src):
+            x = x.to(dst.dtype).reshape(dst.shape)
+            if m is None:
+                dst.copy_(x)
+            else:
+                dst[m] = x[m]
+        mk = m.to(torch.uint8).contiguous() if m is not None else None
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mev_restore_stream_state(self._ctx, C.byref(self._st), _ptr(mk),
+                                                       self._stream()),
+                    "mev_restore_stream_state")
+        self._keep = mk
 
     def set_bs_layout(self, bs_xy, bs_count=None):
         bs = torch.as_tensor(bs_xy, dtype=torch.int32, device=self.device)

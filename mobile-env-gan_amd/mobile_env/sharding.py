@@ -30,12 +30,16 @@ def gather_final(reward, done, group=None):
     import torch.distributed as dist
 
     rd = torch.stack([reward.float(), done.float()])
+    world = dist.get_world_size(group)
     if dist.get_backend(group) == "gloo":  # CPU rehearsal backend
         rd = rd.cpu()
-    world = dist.get_world_size(group)
-    parts = [torch.empty_like(rd) for _ in range(world)]
-    dist.all_gather(parts, rd, group=group)
-    return torch.stack(parts)
+        parts = [torch.empty_like(rd) for _ in range(world)]
+        dist.all_gather(parts, rd, group=group)
+        return torch.stack(parts)
+    # RCCL: one collective straight into the [world, 2, E] result (no per-rank list + stack)
+    out = torch.empty((world,) + tuple(rd.shape), dtype=rd.dtype, device=rd.device)
+    dist.all_gather_into_tensor(out, rd, group=group)
+    return out
 
 
 def gather_obs(obs, group=None):
@@ -46,6 +50,9 @@ def gather_obs(obs, group=None):
     world = dist.get_world_size(group)
     if dist.get_backend(group) == "gloo":
         obs = obs.cpu()
-    parts = [torch.empty_like(obs) for _ in range(world)]
-    dist.all_gather(parts, obs.contiguous(), group=group)
-    return torch.stack(parts)
+        parts = [torch.empty_like(obs) for _ in range(world)]
+        dist.all_gather(parts, obs.contiguous(), group=group)
+        return torch.stack(parts)
+    out = torch.empty((world,) + tuple(obs.shape), dtype=obs.dtype, device=obs.device)
+    dist.all_gather_into_tensor(out, obs.contiguous(), group=group)
+    return out

@@ -211,3 +211,52 @@ def test_c_caller_libm_table_shares_round_like_reference(golden_dir, which):
                                                   err_msg=f"path {path} share count {n}")
         finally:
             L.mev_destroy(ctx)
+
+
+@pytest.mark.parametrize("U,B,launch", [(30, 13, "step"), (30, 13, "rollout"), (100, 24, "step"),
+                                        (100, 24, "rollout")])
+def test_checkpoint_restore_mid_episode(U, B, launch):
+    """A checkpoint {ue_state, pcg (read through the synced property), t} taken mid-episode and
+    restored into a fresh engine with OTHER seeds (restore_state -> mev_restore_stream_state)
+    continues exactly like the saving engine -- across the episode's remaining draws (which
+    come from the restored stream rows, not the new context's draw table) and the next
+    episodes (the tables rebuilt from the restored state0). Velocity 10 on 200 x 200: several
+    waypoint draws per episode. Packed (U = 30) and block (U = 100) shapes, one-step and
+    fused rollout launches. ADVICE r03: without the restore call the new context re-read the
+    episode's first table pairs."""
+    import torch
+    from mobile_env.core.engine import EngineParams, StepEngine
+    rng = np.random.default_rng(7)
+    E = 48
+    bs = rng.integers(0, 200, size=(B, 2)).tolist()
+    p = EngineParams(num_envs=E, num_ues=U, num_bs=B, velocity=10.0)
+    a = StepEngine(p, bs, 1000 + np.arange(E), device="cuda")
+    b = StepEngine(p, bs, 90000 + np.arange(E), device="cuda")
+    c = StepEngine(p, bs, 90000 + np.arange(E), device="cuda")
+    for eng in (a, b, c):
+        eng.reset()
+    a.step(7)
+    ck = (a.ue_state.clone(), a.pcg.clone(), a.t.clone())
+    b.restore_state(*ck)
+    c.ue_state.copy_(ck[0])  # the same rows without the restore call (the bug's shape)
+    c._pcg.copy_(ck[1])
+    c.t.copy_(ck[2])
+    n = 33  # the rest of episode 1 (13 steps) and one more episode
+
+    def run(eng):
+        if launch == "rollout":
+            tr = eng.rollout(n)
+            return [tr.obs.cpu(), tr.serving.cpu(), tr.reward.cpu(), tr.done.cpu()]
+        rows = []
+        for _ in range(n):
+            eng.step()
+            rows.append([eng.obs.cpu(), eng.serving.cpu(), eng.reward.cpu(), eng.done.cpu()])
+        return [torch.stack(col) for col in zip(*rows)]
+
+    ra, rb, rc = run(a), run(b), run(c)
+    for x, y in zip(ra, rb):
+        assert torch.equal(x, y)
+    assert torch.equal(a.ue_state, b.ue_state) and torch.equal(a.pcg, b.pcg)
+    assert not torch.equal(ra[0], rc[0])  # the draw-table replay the restore call prevents
+    for eng in (a, b, c):
+        eng.close()

@@ -104,16 +104,13 @@ def _bench_worker(rank, world, port, out_path):
         reward.copy_(torch.as_tensor(seeds, dtype=torch.float32) + sum(issued))
         done.fill_(int(sum(issued) % 20 == 0))
 
-    class Ev:
-        def record(self):
-            pass
-
     got = {}
 
     def collective():
         got["g"] = gather_final(reward, done)
 
-    elapsed, events = bench.timed_run(issue, plan, lambda: None, dist.barrier, Ev, collective)
+    elapsed, t_steps, t_coll = bench.timed_run(issue, plan, lambda: None, dist.barrier, collective)
+    assert 0 < t_steps <= elapsed and 0 <= t_coll <= elapsed - t_steps + 1e-9
     mine = elapsed
     elapsed = bench.max_over_ranks(elapsed)
     every = [None] * world
@@ -171,3 +168,12 @@ def test_bench_spawns_its_own_ranks():
     assert og["shape"] == [2, E, U, 4] and og["bytes_per_rank"] == E * U * 16
     assert og["checksum"] == float(seeds.sum() * U)
     assert out["value"] == pytest.approx(2 * E * K / (out["ms_per_step"] * K * 1e-3))
+    # both collectives ran once in the untimed warmup (the timed gather is not the first), and
+    # the timed gather's own time and the steps-only rate are reported
+    wg = dd["warmup_gathers"]
+    assert wg is not None and wg["final_ms"] > 0 and wg["obs_ms"] > 0
+    assert 0 < dd["final_gather_ms"] <= out["ms_per_step"] * K
+    assert 0 < dd["final_gather_share"] < 1
+    assert dd["value_steps_only"] >= out["value"]
+    rf = out["roofline"]
+    assert "timed region" in rf["launch_ms_basis"] and rf["launch_ms"] > 0
