@@ -151,6 +151,12 @@ typedef struct mev_params {
    *     in multi-step launches). */
   int32_t lds_tables, two_groups, stage_rows, xcd_remap, scenario_constants, station_culling;
   int32_t ues_per_lane;
+  /* Per-UE velocity (optional, HOST [num_ues], read by mev_create only): UserEquipment u moves
+   * with ue_velocity[u] (entities.py:33-45, movement.py:42-62) instead of `velocity` / its
+   * class's velocity. Velocity drives only the movement, so distinct velocities need no
+   * parameter class: any number of them (one per UE) with the channel classes above limited
+   * to the (snr_tr, noise, height) tuples that differ. All equal: the same as `velocity`. */
+  const double* ue_velocity;
 } mev_params;
 
 typedef struct mev_state {

@@ -134,7 +134,7 @@ __host__ __device__ __forceinline__ KOut out_row(KOut o, int E, int U, int i) {
   return o;
 }
 
-// Movement parameters of one UE class (velocity and the values derived from it on the host).
+// Movement parameters of one UE (velocity and the values derived from it on the host).
 struct MoveP {
   double vel;
   float vel_f, move_lim;
@@ -172,7 +172,7 @@ struct KTables {
   const uint8_t* bs_cls;    // [B] class of station j
   const uint8_t* ue_cls;    // [U] class of UE u
   const int2* pair;         // [NB * NU] {offset into rate_full, d2max} of class pair cb * NU + cu
-  const MoveP* mv;          // [NU] movement parameters per UE class
+  const MoveP* mv;          // [U] movement parameters per UE (its velocity: ue_velocity, else its class's)
   const int16_t* perm;      // [kp.bperm] stations grouped by class (segments of even length,
                             // padded with -1)
   const int* seg;           // [NB + 1] segment bounds in perm
@@ -931,7 +931,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
     }
   }
   if (active) {
-    if (het) move_ue_p(pos, wp, tb.mv[cu]);
+    if (het) move_ue_p(pos, wp, tb.mv[min(u, U - 1)]);
     else move_ue<SCN>(pos, wp, kp);
   }
 
@@ -1476,13 +1476,21 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
   return B + 1 > 64 / G ? B + 1 : 64 / G;
 }
+// A group's context in k_steps_lds2. The per-env flags are wave lane masks (every lane of an env
+// holds its env's bit), changed only inside the wave-uniform draw / reset branch: as per-lane
+// bools the compiler kept them as lane masks anyway and merged them across every divergent
+// region of the step (three s_andn2 / s_and / s_or per flag and group, every step).
+//   sok_w: the env's stream slot holds its stream state (draws past the episode draw table);
+//   mov_w: the env drew past the table in this pair (its state row is stored at the pair end).
 struct Ctx2 {
   int t, drawn;
-  bool s_ok, moved;
+  uint64_t sok_w, mov_w;
   int2 pos, wp;
 };
 
-template <int UC, int SCN, int R, bool PE, bool TF = false>
+// FULL: every env of both groups exists (all pairs but the batch's last partial one): the
+// env / valid lane masks are constants, no per-step mask arithmetic.
+template <int UC, int SCN, int R, bool PE, bool TF = false, bool FULL = false>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
                                           const int (&e)[R], const int (&nok)[R], int kval,
@@ -1506,11 +1514,17 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   uint64_t envok_w[R], valid_w[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    int nk = nok[r];
-    asm volatile("" : "+s"(nk));
-    envok_w[r] = nk >= G ? ~0ull : ((1ull << (uint32_t)(nk * PC)) - 1ull);
-    valid_w[r] = envok_w[r] & kValidPat;
-    env_ok[r] = m.seg < nk;
+    if (FULL) {
+      envok_w[r] = ~0ull;
+      valid_w[r] = kValidPat;
+      env_ok[r] = true;
+    } else {
+      int nk = nok[r];
+      asm volatile("" : "+s"(nk));
+      envok_w[r] = nk >= G ? ~0ull : ((1ull << (uint32_t)(nk * PC)) - 1ull);
+      valid_w[r] = envok_w[r] & kValidPat;
+      env_ok[r] = m.seg < nk;
+    }
   }
   bool valid[R], active[R], need[R], do_reset[R], reset_env[R];
   int tot[R], rank[R];
@@ -1519,7 +1533,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int er = r * G + m.seg;  // the env's slot among the wave's R * G
-    valid[r] = kval < nok[r];
+    valid[r] = FULL ? u < U : kval < nok[r];
     reset_env[r] = env_ok[r] && c[r].t >= KPS(t_end);
     do_reset[r] = reset_env[r] && valid[r];
     rs_w[r] = bal(c[r].t >= KPS(t_end)) & envok_w[r];
@@ -1563,7 +1577,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
         fell_back = true;
         const u128 inc = slot[1];
         u128 s;
-        if (!c[r].s_ok && c[r].drawn > 0) {
+        if (seg_field<PC>(c[r].sok_w, m) == 0u && c[r].drawn > 0) {
           s = at(const_cast<u128*>(tb.tab_st),
                  16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(min(c[r].drawn, M) - 1)));
           wait_vmem();
@@ -1586,12 +1600,18 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // the stream bookkeeping, only where a draw or a reset happened (uniform; without either
     // nothing changes, and the per-lane masks cost ~15 SALU per group)
     if (mneed_w[r] | rs_w[r]) {
-      const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
-                           (do_reset[r] && tot[r] == 0 && u == U - 1);
-      if (fell_back && own_fin) slot[0] = s_fin;
-      if (fell_back && tot[r] > 0) c[r].s_ok = true;
-      else if (tot[r] > 0 || reset_env[r]) c[r].s_ok = false;
-      c[r].moved |= own_fin;
+      // the slot holds the state after draws past the table (fell_back, uniform); a draw from
+      // the table or a reset leaves it to the table: per env, as lane masks (see Ctx2)
+      const uint64_t tw = bal(tot[r] > 0), zw = tw | rs_w[r];
+      if (fell_back) {
+        const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
+                             (do_reset[r] && tot[r] == 0 && u == U - 1);
+        if (own_fin) slot[0] = s_fin;
+        c[r].sok_w = (c[r].sok_w & ~rs_w[r]) | tw;
+        c[r].mov_w |= tw;
+      } else {
+        c[r].sok_w &= ~zw;
+      }
       c[r].drawn += tot[r];
     }
   }
@@ -1977,8 +1997,8 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
     c[r].t = scratch[slot];
     c[r].drawn = scratch[RG + slot];
     // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
-    c[r].s_ok = c[r].drawn > M;
-    c[r].moved = false;
+    c[r].sok_w = bal(c[r].drawn > M);
+    c[r].mov_w = 0;
     const int2 v = make_int2((int)f.s[r].x, (int)f.s[r].y);
     c[r].pos = make_int2((int)(short)v.x, v.x >> 16);
     c[r].wp = make_int2((int)(short)v.y, v.y >> 16);
@@ -2082,16 +2102,26 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         env_ok[r] = (m.seg < G) && (e[r] < kp.E);
         nok[r] = __builtin_amdgcn_readfirstlane(min(max(kp.E - g * G, 0), G));  // envs that exist
       }
-      int i = 0, sr = 0;
-      do {  // (nsteps >= 1: the loop body runs at least once)
-        lds2_step<UC, SCN, R, PE, TF>(kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0,
-                                      lblob, lpcg, hist, ltab, sw + sr * NWG + wvu * G * R,
-                                      dw + sr * NWG + wvu * G * R, lkeys);
-        if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-          flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
-        ++i;
-        sr = sr + 1 == stage_rows ? 0 : sr + 1;
-      } while (i < nsteps);
+      // the pair's steps; a pair whose envs all exist (every pair but the batch's last partial
+      // one) runs the FULL step: constant env masks
+      auto steps = [&](auto full) {
+        int i = 0, sr = 0;
+        do {  // (nsteps >= 1: the loop body runs at least once)
+          lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
+              kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
+              sw + sr * NWG + wvu * G * R, dw + sr * NWG + wvu * G * R, lkeys);
+          if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
+            flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+          ++i;
+          sr = sr + 1 == stage_rows ? 0 : sr + 1;
+        } while (i < nsteps);
+      };
+#ifdef MEV_LDS2_FULL
+      if (nok[R - 1] == G) steps(std::true_type{});
+      else steps(std::false_type{});
+#else
+      steps(std::false_type{});
+#endif
       MEV_TS(min(3 + 3 * it, 27));
       // the state after the last step (see k_steps_packed), as unconditional buffer stores; the
       // stream state only where the slot holds it (draws past the table, mev_state.pcg): no
@@ -2103,7 +2133,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         const v2u32 pv = {(unsigned)pw.x, (unsigned)pw.y};
         __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
                                               env_ok[r] && m.u < U ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
-        const bool mvd = seg_field<PC>(bal(c[r].moved), m) != 0u;
+        const bool mvd = seg_field<PC>(c[r].mov_w, m) != 0u;
         const bool ld = env_ok[r] && leader;
         __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].t, out_rsrc(st.t, bt),
                                               ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
@@ -2113,7 +2143,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         const v4u32 sv = {(unsigned)(uint64_t)sl, (unsigned)((uint64_t)sl >> 32),
                           (unsigned)(uint64_t)(sl >> 64), (unsigned)((uint64_t)(sl >> 64) >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(sv, out_rsrc(st.pcg, 12u * bt),
-                                               ld && mvd && c[r].s_ok ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
+                                               ld && mvd && seg_field<PC>(c[r].sok_w, m) != 0u
+                                                   ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
       }
     }
     if (nxt_ok) {  // the next pair's inputs (waited for: free after a whole pair's stores)
@@ -2506,7 +2537,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       reinterpret_cast<unsigned char*>(lds_raw + block_lds_bytes(KPS(B), KPS(tab_m)));
   // heterogeneous entities (UPL 1): this UE's class and movement parameters
   const int cu = HET ? (valid[0] ? (int)tb.ue_cls[tid] : 0) : 0;
-  const MoveP mp = HET ? tb.mv[cu]
+  const MoveP mp = HET ? tb.mv[valid[0] ? tid : 0]
                        : MoveP{kp.vel, KPSF(vel_f), KPSF(move_lim), KPS(d2snap), KPS(axis_exact)};
   // one workgroup per env (grid = E): no loop over envs, whose loop-invariant values the
   // compiler would hoist and spill under the 64-VGPR budget (76 B of scratch per lane, written
@@ -3323,6 +3354,8 @@ static int validate(const mev_params* p) {
     return MEV_EINVAL;
   if (p->rate_table && (p->rate_table_len < 0 || p->rate_table_len > kD2Top + 1))
     return MEV_EINVAL;
+  for (int u = 0; p->ue_velocity && u < p->num_ues; ++u)
+    if (!(p->ue_velocity[u] >= 0.0) || !std::isfinite(p->ue_velocity[u])) return MEV_EINVAL;
   if (p->num_bs_classes < 0 || p->num_ue_classes < 0 || p->num_bs_classes > kMaxClasses ||
       p->num_ue_classes > kMaxClasses)
     return MEV_EINVAL;
@@ -3673,7 +3706,9 @@ static MoveP host_move_params(double velocity, int W, int H) {
   return mp;
 }
 
-static bool is_het(const mev_params* p) { return p->num_bs_classes > 1 || p->num_ue_classes > 1; }
+static bool is_het(const mev_params* p) {
+  return p->num_bs_classes > 1 || p->num_ue_classes > 1 || p->ue_velocity != nullptr;
+}
 
 // Heterogeneous entities: class arrays, per-pair channel tables (the caller's, else libm per
 // pair), per-UE-class movement parameters, stations grouped by class. Fills c->rate_full and
@@ -3720,10 +3755,13 @@ static int build_het(mev_ctx* c) {
       kp.d2max = std::max(kp.d2max, (int)n - 1);
     }
   all.push_back(0.0);  // (never indexed; keeps the buffer non-empty)
-  std::vector<MoveP> mv(NU);
-  for (int cu = 0; cu < NU; ++cu)
-    mv[cu] = host_move_params(p->ue_class_params ? p->ue_class_params[4 * cu] : p->velocity,
-                              p->width, p->height);
+  // movement parameters per UE: its own velocity (ue_velocity), else its class's; distinct
+  // velocities need no class (velocity only drives movement, movement.py:42-62)
+  std::vector<MoveP> mv(U);
+  for (int u = 0; u < U; ++u)
+    mv[u] = host_move_params(p->ue_velocity ? p->ue_velocity[u]
+                             : p->ue_class_params ? p->ue_class_params[4 * ucl[u]] : p->velocity,
+                             p->width, p->height);
   // stations grouped by class, each segment padded to an even length (pairs of keys)
   std::vector<int16_t> perm;
   std::vector<int> seg(NB + 1, 0);
@@ -3790,6 +3828,15 @@ static bool packed_shape(const mev_ctx* c) {
 static int create_ctx(mev_ctx* c, const mev_params* params) {
   int rc = 0;
   c->p = *params;
+  if (c->p.ue_velocity) {  // one velocity for every UE: the homogeneous kernels
+    bool same = true;
+    for (int u = 1; u < c->p.num_ues; ++u) same = same && c->p.ue_velocity[u] == c->p.ue_velocity[0];
+    if (same) {
+      c->p.velocity = c->p.ue_velocity[0];
+      c->p.ue_velocity = nullptr;
+    }
+  }
+  params = &c->p;  // (normalised; ue_velocity is read only while creating)
   MEV_HIP(hipGetDevice(&c->device));
 
   KParams& kp = c->kp;

@@ -53,6 +53,7 @@ class MevParams(C.Structure):
         ("xcd_remap", C.c_int32), ("scenario_constants", C.c_int32),
         ("station_culling", C.c_int32),
         ("ues_per_lane", C.c_int32),
+        ("ue_velocity", C.c_void_p),
     ]
 
 

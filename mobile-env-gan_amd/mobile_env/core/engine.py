@@ -70,9 +70,14 @@ class EngineParams:
     ue_classes: "list | None" = None   # [{velocity, snr_tr, noise, height}]
     bs_class: "list | None" = None     # [B] class index per station
     ue_class: "list | None" = None     # [U] class index per UE
+    # per-UE velocity (mev_params.ue_velocity; None: `velocity` / the UE's class's): velocity
+    # drives only the movement, so any number of distinct values needs no class
+    ue_velocity: "list | None" = None  # [U]
 
     @property
     def heterogeneous(self) -> bool:
+        """More than one channel class on a side (the per-pair tables; per-UE velocities alone
+        need none: see ue_velocity)."""
         return len(self.bs_classes or ()) > 1 or len(self.ue_classes or ()) > 1
 
     def _classes(self):
@@ -145,7 +150,9 @@ class EngineParams:
             lds_tables=int(self.lds_tables), two_groups=int(self.two_groups),
             stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
             scenario_constants=int(self.scenario_constants),
-            station_culling=int(self.station_culling), ues_per_lane=int(self.ues_per_lane))
+            station_culling=int(self.station_culling), ues_per_lane=int(self.ues_per_lane),
+            ue_velocity=(arr([float(v) for v in self.ue_velocity], np.float64)
+                         if self.ue_velocity is not None else C.c_void_p(None)))
         cp._keep = keep
         return cp
 

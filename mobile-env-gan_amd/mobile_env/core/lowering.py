@@ -71,27 +71,33 @@ def lower(*, num_envs, stations, users, arrival, channel, scheduler, movement, u
           ep_max_time, first_step_active) -> EngineParams:
     """Flat engine parameters. Entities with different parameters (the reference keeps them
     per BaseStation / UserEquipment, entities.py:7-22,33-45) lower to parameter classes: one
-    channel table per (station class, UE class) pair and the movement velocity per UE class."""
+    channel table per (station class, UE class) pair, the classes over the channel-relevant
+    values only; the velocity (movement only, movement.py:42-62) goes per UE, any number of
+    distinct values."""
     check_plugins(arrival, channel, scheduler, movement, utility)
     bsc, bsi = _classes([(s.bw, s.frequency, s.tx_power, s.height) for s in stations])
-    uec, uei = _classes([(u.velocity, u.snr_threshold, u.noise, u.height) for u in users])
+    uec, uei = _classes([(u.snr_threshold, u.noise, u.height) for u in users])
+    vels = [float(u.velocity) for u in users]
     if len(bsc) > 16 or len(uec) > 16:
-        raise NotImplementedError("more than 16 station or UE parameter classes")
+        raise NotImplementedError("more than 16 station or UE channel parameter classes "
+                                  "(distinct (bw, freq, tx, height) / (snr_tr, noise, height))")
     mv = movement.lower_params()
     ar = arrival.lower_params()
     ut = utility.lower_params()
     bs_dicts = [{"bw": b[0], "freq": b[1], "tx": b[2], "height": b[3]} for b in bsc]
-    ue_dicts = [{"velocity": float(u[0]), "snr_tr": u[1], "noise": u[2], "height": u[3]}
-                for u in uec]
+    ue_dicts = [{"velocity": vels[uei.index(c)], "snr_tr": u[0], "noise": u[1], "height": u[2]}
+                for c, u in enumerate(uec)]
     het = len(bsc) > 1 or len(uec) > 1
+    per_ue_vel = len(set(vels)) > 1
     return EngineParams(
         num_envs=num_envs, num_ues=len(users), num_bs=len(stations),
         width=mv["width"], height=mv["height"], ep_max_time=int(ep_max_time),
         arrival_start=ar["arrival_start"], arrival_exit=ar["arrival_exit"],
         first_step_active=first_step_active, movement_reseed=mv["movement_reseed"],
-        velocity=float(uec[0][0]), bs=bs_dicts[0],
+        velocity=vels[0], bs=bs_dicts[0],
         ue={k: ue_dicts[0][k] for k in ("snr_tr", "noise", "height")},
         util_lower=ut["util_lower"], util_upper=ut["util_upper"], util_coeffs=ut["util_coeffs"],
         draw_table=0,  # the facade carries pcg / t across engine rebuilds: no episode table
         bs_classes=bs_dicts if het else None, ue_classes=ue_dicts if het else None,
-        bs_class=bsi if het else None, ue_class=uei if het else None)
+        bs_class=bsi if het else None, ue_class=uei if het else None,
+        ue_velocity=vels if per_ue_vel else None)

@@ -47,6 +47,9 @@ class OracleParams:
     ue_classes: list = None
     bs_class: list = None
     ue_class: list = None
+    # per-UE velocities (the reference's UserEquipment.velocity, entities.py:33-45; overrides
+    # `velocity` / the UE classes' velocity)
+    ue_velocity: list = None
 
     @property
     def t_end(self) -> int:
@@ -123,6 +126,8 @@ class OracleBatch:
             self.pair_id = bcl[:, None] * len(uec) + ucl[None, :]
             self.pair_d2max = np.asarray(d2m, dtype=np.int64)[self.pair_id]
             self.vel = np.asarray([float(uec[c]["velocity"]) for c in ucl])
+        if p.ue_velocity is not None:
+            self.vel = np.asarray(p.ue_velocity, dtype=np.float64).reshape(self.U)
         self.t = np.full(self.E, p.t_end, dtype=np.int64)   # "episode over": next step resets
         self.x = np.zeros((self.E, self.U), dtype=np.int64)
         self.y = np.zeros((self.E, self.U), dtype=np.int64)

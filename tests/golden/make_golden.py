@@ -446,12 +446,167 @@ def main():
     print("wrote", sorted(out) + [f"channel_{t}" for t in tables])
 
 
+def _build_cfg(ref_base, BaseStation, UserEquipment, bs_xy, bs_params, ue_params, seed, extra):
+    """FixedCore over stations / UEs with per-entity kwargs (lists) and config overrides (map
+    size: "width" / "height" and movement_params, base.py:104-108,130-134)."""
+    build = _make_fixed_core(ref_base, BaseStation, UserEquipment)
+    env, _ = build(bs_xy, len(ue_params), seed)  # for the FixedCore class
+    stations = [BaseStation(i, (int(x), int(y)), **bs_params[i]) for i, (x, y) in enumerate(bs_xy)]
+    users = [UserEquipment(i, **ue_params[i]) for i in range(len(ue_params))]
+    cfg = {"seed": seed}
+    cfg.update(json.loads(json.dumps(extra)))
+    return type(env)(stations, users, cfg), users
+
+
+def _map_cfg(w, h):
+    return {"width": w, "height": h, "movement_params": {"width": w, "height": h}}
+
+
+# Round-4 fixtures (--wide): maps wider than 200, a tx = 55 channel, stations outside the map,
+# per-env layouts, U > 64, heterogeneous classes on a 4,096 map; and per-UE velocities
+# (30 distinct values) with a per-UE snr_tr spread. name -> (W, H, layouts [E] of [B][2] or one
+# shared [B][2], U, bs kwargs per station (or one dict), ue kwargs per UE (or one dict), seeds,
+# episodes)
+def wide_plans():
+    r = np.random.default_rng(1500)
+    lay1500 = r.integers(0, 1500, size=(11, 2)).tolist() + [[1600, 200], [3000, 1400]]
+    r = np.random.default_rng(4096)
+    lay4096 = r.integers(0, 4096, size=(13, 2)).tolist()
+    per_env = [np.random.default_rng(40 + k).integers(0, 4096, size=(9 + 2 * k, 2)).tolist()
+               for k in range(3)]
+    bs_def = {"bw": 9e6, "freq": 2500, "tx": 40, "height": 50}
+    bs55 = dict(bs_def, tx=55)
+    ue_def = {"velocity": 1.5, "snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
+    bs_cls = [dict(bs55), {"bw": 9e6, "freq": 2500, "tx": 45, "height": 50},
+              {"bw": 5e6, "freq": 1800, "tx": 50, "height": 30}]
+    ue_cls = [dict(ue_def, velocity=60), {"velocity": 40, "snr_tr": 2e-8, "noise": 1e-9,
+                                          "height": 1.8},
+              {"velocity": 25, "snr_tr": 1e-7, "noise": 2e-9, "height": 1.5}]
+    snr_spread = [2e-8, 5e-8, 1e-7, 1e-8]
+    return {
+        "wide1500": (1500, 1500, lay1500, 30, bs_def, ue_def, [2024, 9], 2),
+        "wide4096_tx55": (4096, 4096, lay4096, 30, bs55, dict(ue_def, velocity=60),
+                          [2024, 9], 2),
+        "wide4096_tx55_perenv": (4096, 4096, per_env, 30, bs55, dict(ue_def, velocity=60),
+                                 [3, 4, 5], 2),
+        "wide1500_block": (1500, 1500, lay1500, 100, bs_def, dict(ue_def, velocity=10), [5],
+                           2),
+        "wide4096_mixed": (4096, 4096, lay4096, 30, [bs_cls[i % 3] for i in range(13)],
+                           [ue_cls[(i * 7) % 3] for i in range(30)], [3, 2024], 2),
+        # per-UE velocities (all distinct) and snr_tr from a 4-value spread, default map
+        "velocities_large": (200, 200, None, 30, bs_def,
+                             [dict(ue_def, velocity=1.0 + 0.75 * i,
+                                   snr_tr=snr_spread[(i * 3) % 4]) for i in range(30)],
+                             [2024, 77], 2),
+    }
+
+
+def wide_fixtures(ref_base, BaseStation, UserEquipment, OkumuraHata):
+    layouts = json.load(open(LAYOUTS))
+    out = {}
+    for name, (W, H, lay, U, bsp, uep, seeds, episodes) in wide_plans().items():
+        if lay is None:
+            lay = layouts["large"]["bs"]
+        per_env = isinstance(lay[0][0], list)
+        runs = []
+        for k, sd in enumerate(seeds):
+            L = lay[k] if per_env else lay
+            bl = bsp if isinstance(bsp, list) else [bsp] * len(L)
+            ul = uep if isinstance(uep, list) else [uep] * U
+            env, users = _build_cfg(ref_base, BaseStation, UserEquipment, L, bl, ul, sd,
+                                    _map_cfg(W, H))
+            runs.append(run_episodes(env, users, episodes=episodes, steps=20))
+        rec = {k: np.stack([r[k] for r in runs]) for k in runs[0]}
+        if per_env:
+            Bm = max(len(x) for x in lay)
+            bs_xy = np.full((len(lay), Bm, 2), 0, dtype=np.int64)
+            for k, x in enumerate(lay):
+                bs_xy[k, :len(x)] = x
+            extra = dict(bs_xy=bs_xy, bs_count=np.asarray([len(x) for x in lay]))
+        else:
+            extra = dict(bs_xy=np.asarray(lay, dtype=np.int64))
+        out[name] = dict(
+            width=np.int64(W), height=np.int64(H), seeds=np.asarray(seeds, dtype=np.int64),
+            bs_params=json.dumps(bsp), ue_params=json.dumps(uep),
+            velocity=np.float64(uep["velocity"] if isinstance(uep, dict) else np.nan),
+            **extra, **rec)
+        print(name, "serving share", float((rec["serving"] >= 0).mean()))
+    # the tx = 55 channel at every integer d2 up to its d2max (+1: not connectable)
+    bsp = wide_plans()["wide4096_tx55"][4]
+    uep = {"snr_tr": 2e-8, "noise": 1e-9, "height": 1.6}
+    hi = 2 * 1023 * 1023
+    lo, top = 0, hi
+    while lo < top:  # the last connectable d2 (connectivity is a prefix: checked below)
+        mid = (lo + top + 1) // 2
+        snr, _ = rate_table_range(OkumuraHata, bsp, uep, mid, mid)
+        if snr[0] > uep["snr_tr"]:
+            lo = mid
+        else:
+            top = mid - 1
+    d2max = lo
+    snr, rate = rate_table_range(OkumuraHata, bsp, uep, 0, d2max + 1)
+    conn = snr > uep["snr_tr"]
+    assert conn[: d2max + 1].all() and not conn[d2max + 1:].any(), "connectivity not a prefix"
+    out["channel_tx55"] = dict(d2max=np.int64(d2max), rate=rate[: d2max + 1],
+                               snr_margin=np.float64(np.min(np.abs(snr / uep["snr_tr"] - 1.0))),
+                               bs=json.dumps(bsp), ue=json.dumps(uep))
+    print("channel_tx55 d2max", d2max)
+    return out
+
+
+def rate_table_range(OkumuraHata, bs_params, ue_params, d2_lo, d2_hi):
+    """rate_table over [d2_lo, d2_hi] only."""
+
+    class _P:
+        def __init__(self, d2):
+            self.d2 = d2
+
+        def distance(self, other):
+            return math.sqrt(other.d2)
+
+    class _BS:
+        point = _P(0)
+        bw = bs_params["bw"]
+        frequency = bs_params["freq"]
+        tx_power = bs_params["tx"]
+        height = bs_params["height"]
+
+    class _UE:
+        height = ue_params["height"]
+        noise = ue_params["noise"]
+        snr_threshold = ue_params["snr_tr"]
+
+    ch = OkumuraHata()
+    ue = _UE()
+    n = d2_hi - d2_lo + 1
+    snr = np.empty(n)
+    rate = np.empty(n)
+    for i in range(n):
+        ue.point = _P(d2_lo + i)
+        s = ch.calculateSNR(_BS, ue)
+        snr[i] = float(s)
+        rate[i] = float(ch.datarate(_BS, ue, s))
+    return snr, rate
+
+
+def main_wide():
+    ref_base, BaseStation, UserEquipment, OkumuraHata, ref_custom = _import_reference()
+    scratch = tempfile.mkdtemp(prefix="mev_golden_")
+    os.chdir(scratch)
+    for name, arrs in wide_fixtures(ref_base, BaseStation, UserEquipment, OkumuraHata).items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+        print("wrote", name)
+
+
 if __name__ == "__main__":
     # --extra: only the round-2 fixtures (per-env 128 x 1024, heterogeneous parameters);
-    # --knobs: only the round-3 config-knob fixtures (KNOBS)
+    # --knobs: only the round-3 config-knob fixtures (KNOBS); --wide: only the round-4 wide-map /
+    # tx 55 / per-UE velocity fixtures (wide_plans)
     if "--extra" in sys.argv[1:]:
         main_extra()
     elif "--knobs" in sys.argv[1:]:
         main_knobs()
+    elif "--wide" in sys.argv[1:]:
+        main_wide()
     else:
         main()

@@ -130,3 +130,64 @@ def knob_done(d):
     done = np.zeros(int(lens.sum()), dtype=bool)
     done[ends] = True
     return done
+
+
+# Round-4 reference fixtures (tests/golden/make_golden.py --wide): maps wider than 200, a tx 55
+# channel, per-env layouts, U > 64, classes on a 4,096 map, per-UE velocities
+WIDE_FIXTURES = ("wide1500", "wide4096_tx55", "wide4096_tx55_perenv", "wide1500_block",
+                 "wide4096_mixed", "velocities_large")
+
+
+def fixture_entities(d):
+    """Parameters of a --wide fixture: (bs dict, ue dict incl. velocity) when every entity has
+    the same, else the per-entity lists as parameter classes {bs_classes, ue_classes, bs_class,
+    ue_class} (unique tuples in first-appearance order)."""
+    bsp, uep = json.loads(str(d["bs_params"])), json.loads(str(d["ue_params"]))
+
+    def classes(lst, keys):
+        uniq, idx = [], []
+        for x in lst:
+            t = tuple(x[k] for k in keys)
+            if t not in uniq:
+                uniq.append(t)
+            idx.append(uniq.index(t))
+        return [dict(zip(keys, t)) for t in uniq], idx
+
+    out = {}
+    if isinstance(bsp, list):
+        out["bs_classes"], out["bs_class"] = classes(bsp, ("bw", "freq", "tx", "height"))
+        if len(out["bs_classes"]) == 1:
+            del out["bs_classes"], out["bs_class"]
+        bsp = bsp[0]
+    if isinstance(uep, list):
+        # channel classes over (snr_tr, noise, height); velocities per UE (mev_params.ue_velocity)
+        vel = [float(u["velocity"]) for u in uep]
+        out["ue_classes"], out["ue_class"] = classes(uep, ("snr_tr", "noise", "height"))
+        for c in out["ue_classes"]:
+            c["velocity"] = vel[out["ue_class"].index(out["ue_classes"].index(c))]
+        if len(out["ue_classes"]) == 1:
+            del out["ue_classes"], out["ue_class"]
+        if len(set(vel)) > 1:
+            out["ue_velocity"] = vel
+        uep = uep[0]
+    return bsp, uep, out
+
+
+def wide_oracle(d, table=None):
+    from oracle.vec import OracleBatch, OracleParams
+    bsp, uep, cls = fixture_entities(d)
+    p = OracleParams(width=int(d["width"]), height=int(d["height"]),
+                     velocity=float(uep["velocity"]), bs=dict(bsp),
+                     ue={k: uep[k] for k in ("snr_tr", "noise", "height")}, **cls)
+    cnt = d["bs_count"] if "bs_count" in d else None
+    return OracleBatch(p, d["bs_xy"], d["xy"].shape[2], d["seeds"], bs_count=cnt, table=table)
+
+
+def wide_engine_params(d, **kw):
+    from mobile_env.core.engine import EngineParams
+    bsp, uep, cls = fixture_entities(d)
+    return EngineParams(num_envs=len(d["seeds"]), num_ues=int(d["xy"].shape[2]),
+                        num_bs=int(d["bs_xy"].shape[-2]), width=int(d["width"]),
+                        height=int(d["height"]), velocity=float(uep["velocity"]),
+                        bs=dict(bsp), ue={k: uep[k] for k in ("snr_tr", "noise", "height")},
+                        **cls, **kw)

@@ -159,11 +159,21 @@ def test_lowering_builtin_plugins_and_rejects_others():
     st[1].tx_power = 30
     p = lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
                        first_step_active=True, **plug)
-    assert p.heterogeneous and p.bs_class == [0, 1, 0] and p.ue_class == [0, 0, 1, 0]
+    assert p.heterogeneous and p.bs_class == [0, 1, 0] and p.ue_class == [0, 0, 0, 0]
     assert [c["tx"] for c in p.bs_classes] == [40, 30]
-    assert [c["velocity"] for c in p.ue_classes] == [1.5, 3.0]
+    # the velocity goes per UE (movement only): no UE class for it
+    assert p.ue_velocity == [1.5, 1.5, 3.0, 1.5] and len(p.ue_classes) == 1
+    us[1].snr_threshold = 5e-8
+    p = lowering.lower(num_envs=1, stations=st, users=us, ep_max_time=20,
+                       first_step_active=True, **plug)
+    assert p.ue_class == [0, 1, 0, 0] and [c["snr_tr"] for c in p.ue_classes] == [2e-8, 5e-8]
     tab, offs = p.rate_table()
     assert len(offs) == 2 * 2 + 1 and offs[-1] == len(tab)
+    # any number of distinct velocities (the 16-class limit is on the channel tuples only)
+    us2 = [UserEquipment(i, 1.0 + 0.5 * i, 2e-8, 1e-9, 1.6) for i in range(40)]
+    p = lowering.lower(num_envs=1, stations=st, users=us2, ep_max_time=20,
+                       first_step_active=True, **plug)
+    assert p.ue_velocity == [1.0 + 0.5 * i for i in range(40)]
 
 
 def test_mcom_custom_layout_uses_global_random_like_reference():

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 from hypothesis import given, settings, strategies as st
 
-from helpers import FIXTURES, load, snapshots
+from helpers import FIXTURES, WIDE_FIXTURES, load, snapshots
 from oracle import port
 from oracle.vec import OracleBatch, OracleParams, channel_table, snr_scalar
 
@@ -255,3 +255,37 @@ def test_reference_channel_tables_share_tie_free(golden_dir):
         for n in range(1, 1025):
             np.testing.assert_array_equal(np.rint(r * (100.0 / n)), np.rint((r / n) * 100.0),
                                           err_msg=f"{name} n={n}")
+
+
+@pytest.mark.parametrize("name", WIDE_FIXTURES)
+def test_vec_oracle_matches_wide_fixture(name):
+    """Maps wider than 200 (1,500^2 / 4,096^2, stations beyond the map's edge included), the
+    tx = 55 channel, per-env layouts on a 4,096 map, U = 100, parameter classes on a 4,096 map
+    and 30 distinct per-UE velocities with a per-UE snr_tr spread: the oracle reproduces the
+    reference's fixtures (make_golden.py --wide) bit for bit -- positions (the int(W u)
+    waypoint draws at W = 4,096, the float step of velocities 1.5 to 60), serving stations,
+    rates (the tx 55 channel chain), utilities, metrics."""
+    from helpers import wide_oracle
+    d = load(name)
+    ob = wide_oracle(d)
+    for s in range(d["xy"].shape[1]):
+        o = ob.step()
+        np.testing.assert_array_equal(o["xy"], d["xy"][:, s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(o["serving"], d["serving"][:, s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(o["rate"], d["rate"][:, s], err_msg=f"step {s}")
+        act = ~np.isnan(d["util"][:, s])
+        np.testing.assert_array_equal(np.isnan(o["util"]), ~act)
+        np.testing.assert_array_equal(o["util"][act], d["util"][:, s][act])
+        np.testing.assert_array_equal(o["metrics"][:, :3], d["metrics"][:, s, :3])
+        np.testing.assert_allclose(o["metrics"][:, 3], d["metrics"][:, s, 3], rtol=1e-12)
+
+
+def test_channel_table_tx55_matches_reference(golden_dir):
+    """The tx = 55 channel (the wide-map fixtures' stations) at every integer d2 up to its
+    d2max = 149,716 (d2max + 1 not connectable): the oracle's table is the reference's."""
+    c = np.load(f"{golden_dir}/channel_tx55.npz")
+    p = OracleParams(width=4096, height=4096, bs={"bw": 9e6, "freq": 2500, "tx": 55,
+                                                  "height": 50})
+    d2max, rate = channel_table(p)
+    assert d2max == int(c["d2max"]) == 149716
+    np.testing.assert_array_equal(rate, c["rate"])

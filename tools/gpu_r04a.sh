@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 GPU session A: the GPU test suite, 20-step timeline probe, kernel-variant A/B.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -v -m gpu --maxfail=10 --timeout 150 --timeout-method thread \
+  > gpurun_out/pytest_r04a.log 2>&1
+rc=$?
+grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_r04a.log | tail -15
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+MEV_LIB=$PWD/mobile-env-gan_amd/lib/libmev_ts.so REPS=5 timeout -k 10 150 python -u tools/ts_probe.py 20 > gpurun_out/ts_base.log 2>&1 || exit 1
+VARIANTS="${VARIANTS:-base flags full nt sc1}" REPS=3 LENS="20 200" bash tools/ab.sh
