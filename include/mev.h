@@ -22,7 +22,9 @@
  *   - Layout (SoA, row-major, E envs, U UEs, B base stations per env):
  *       ue_state int16 [E][U][4]  {x, y, wx, wy}: UE position (integer grid,
  *                                 entities.py:52-54) and RandomWaypoint target
- *                                 (movement.py:44-47); wx < 0 means "no waypoint"
+ *                                 (movement.py:44-47); wx < 0 means "no waypoint";
+ *                                 or uint8 [E][U][4] with 255 for -1 (compact_state,
+ *                                 maps <= 255 per side; mev_state_bytes_per_ue)
  *       pcg     uint64[E][6]      numpy-PCG64 stream of the movement model:
  *                                 {state_lo, state_hi, inc_lo, inc_hi,
  *                                  state0_lo, state0_hi}; state0 = state right after
@@ -59,7 +61,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 19
+#define MEV_ABI_VERSION 20
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -157,10 +159,14 @@ typedef struct mev_params {
    * parameter class: any number of them (one per UE) with the channel classes above limited
    * to the (snr_tr, noise, height) tuples that differ. All equal: the same as `velocity`. */
   const double* ue_velocity;
+  /* 1: the compact UE state form, ue_state = uint8 [E][U][4] {x, y, wx, wy} with 255 for -1
+   * (no waypoint) -- half the state bytes, which one-step launches move every step; maps up to
+   * 255 per side only (every registered scenario is 200 x 200). 0: int16 [E][U][4]. */
+  int32_t compact_state;
 } mev_params;
 
 typedef struct mev_state {
-  int16_t* ue_state;
+  int16_t* ue_state;      /* (uint8_t* with compact_state) */
   uint64_t* pcg;
   int32_t* t;
   const int32_t* bs_xy;
@@ -206,6 +212,8 @@ int mev_step_shape(const mev_ctx* ctx);
 /* Bytes of the compact association tables rollout launches copy into LDS (shared layouts whose
  * tables fit); 0: rollouts gather from the L2 association map. */
 int mev_lds_tables_bytes(const mev_ctx* ctx);
+/* Bytes of one UE's ue_state row: 4 (compact_state, uint8 x4) or 8 (int16 x4). */
+int mev_state_bytes_per_ue(const mev_ctx* ctx);
 /* Device pointer to the channel rate table (float64 [d2max+1]) -- for tests. */
 const double* mev_rate_table(const mev_ctx* ctx);
 /* Copy the first n entries of the channel rate table to dst (host or device memory,

@@ -99,10 +99,12 @@ struct KParams {
   // block kernel station culling (0: off): cells of 2^cull_log x 2^cull_log, cull_nx per row,
   // cull_nc in all (block_cull_params)
   int cull_log, cull_nx, cull_nc;
+  int st8;            // compact UE state: uint8 x4 per UE (maps <= 255 per side; 255 = -1)
 };
 
 struct KState {
-  int2* ue_state;  // [E][U] {x, y, wx, wy} as int16x4 (8 B per UE; coordinates < 1024, -1)
+  int2* ue_state;  // [E][U] {x, y, wx, wy} as int16x4 (8 B per UE; coordinates < 4096, -1), or
+                   // with KParams::st8 as uint8 x4 (4 B per UE; 255 = -1: no waypoint)
   uint64_t* pcg;
   int* t;
   const int2* bs_xy;
@@ -201,6 +203,29 @@ __device__ __forceinline__ void store_ue(int2* p, int2 pos, int2 wp) {
                  (int)(((unsigned)wp.x & 0xffffu) | ((unsigned)wp.y << 16)));
 }
 
+// Compact UE state (KParams::st8, maps <= 255 per side): {x, y, wx, wy} as uint8 x4, one 4-byte
+// load / store per UE (half the state bytes of the int16 form: the one-step launches move the
+// state every step); 255 encodes -1 (no waypoint).
+__device__ __forceinline__ int dec8(unsigned b) { return b == 255u ? -1 : (int)b; }
+__device__ __forceinline__ unsigned pack8(int2 pos, int2 wp) {
+  return ((unsigned)pos.x & 255u) | (((unsigned)pos.y & 255u) << 8) |
+         (((unsigned)wp.x & 255u) << 16) | ((unsigned)wp.y << 24);
+}
+__device__ __forceinline__ int4 unpack8(unsigned v) {
+  return make_int4((int)(v & 255u), (int)((v >> 8) & 255u), dec8((v >> 16) & 255u),
+                   dec8(v >> 24));
+}
+// UE ui's state row in either form (`st8` wave-uniform, a compile-time constant in the
+// scenario instances)
+__device__ __forceinline__ int4 load_ue_at(int2* base, uint32_t ui, bool st8) {
+  if (st8) return unpack8(at(reinterpret_cast<unsigned*>(base), 4u * ui));
+  return load_ue(&at(base, 8u * ui));
+}
+__device__ __forceinline__ void store_ue_at(int2* base, uint32_t ui, int2 pos, int2 wp, bool st8) {
+  if (st8) at(reinterpret_cast<unsigned*>(base), 4u * ui) = pack8(pos, wp);
+  else store_ue(&at(base, 8u * ui), pos, wp);
+}
+
 // ------------------------------------------------------------------------------------
 // PCG64 helpers (device)
 // ------------------------------------------------------------------------------------
@@ -278,7 +303,10 @@ __host__ __device__ constexpr ScnConst scn_const(int scn) {
                              19362, 2, 50, 2500}
                   : ScnConst{};
 }
+// every registered scenario is a 200 x 200 map: compact state (the host sets st8 there)
+__host__ __device__ constexpr bool scn_st8(int scn) { return scn >= 1 && scn <= 4; }
 #define KPS(f) (SCN ? scn_const(SCN).f : kp.f)
+#define KST8 (SCN ? scn_st8(SCN) : kp.st8 != 0)
 #define KPSF(f) (SCN ? __builtin_bit_cast(float, scn_const(SCN).f) : kp.f)
 
 // Per-UE movement (movement.py:42-62), exact float64 form: the reference computes
@@ -583,6 +611,7 @@ struct GroupIn {
   ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
 };
 
+template <int SCN = 0>
 __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& st,
                                               const KTables& tb, int e, int u, int U,
                                               bool fused) {
@@ -590,7 +619,7 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
   g.t = at(st.t, 4u * (uint32_t)ec);
-  g.s = load_ue(&at(st.ue_state, 8u * ue));
+  g.s = load_ue_at(st.ue_state, ue, KST8);
   if (fused || kp.tab_m) {  // the stream state is read only where a draw needs it (fused:
     g.drawn = kp.tab_m ? at(tb.drawn, 4u * (uint32_t)ec) : 0;  // the caller's LDS slot)
     // the state row is the stream state without a table, or after draws past it
@@ -625,7 +654,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_reset_packed(KParams kp, KStat
   int x, y;
   const u128 s_fin = pcg_draw_pair(s0, inc, 2 * m.u, tb.jump, kp.Wd, kp.Hd, x, y);
   const size_t idx = (size_t)e * kp.U + m.u;
-  store_ue(st.ue_state + idx, make_int2(x, y), make_int2(-1, -1));
+  store_ue_at(st.ue_state, (uint32_t)idx, make_int2(x, y), make_int2(-1, -1), kp.st8 != 0);
   out.serving[idx] = -1;
   out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
   if (out.rate64) out.rate64[idx] = 0.0;
@@ -1130,7 +1159,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   const double util_out = active ? util : __builtin_nan("");
   if (valid && !FUSED) {
     const uint32_t ui = (uint32_t)idx;
-    store_ue(&at(st.ue_state, 8u * ui), pos, wp);
+    store_ue_at(st.ue_state, ui, pos, wp, KST8);
     at(out.serving, 4u * ui) = srv;
     at(out.obs, 16u * ui) = obs;
     if (own_fin && (!M || fell_back))  // the stream moved: write the new state back (with the
@@ -1264,7 +1293,7 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const int e = g * G + m.seg;
   const bool env_ok = (m.seg < G) && (e < kp.E);
   if (g < ngroups) {
-    GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, false);
+    GroupIn a = load_group<SCN>(kp, st, tb, e, min(m.u, U - 1), U, false);
     packed_group<PER_ENV_BS, LEAN, UC, false, 0, SCN, STG>(
         kp, st, out, tb, m, a, e, env_ok, lds_hist + (threadIdx.x >> 6) * G * kp.B, nullptr,
         nullptr, 0, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
@@ -1378,7 +1407,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
       for (int c = 0; c * 64 < lim; ++c)
         if (c * 64 + lane < lim) glds(src + c * 64 + lane, ltab + c * 64);
     }
-    GroupIn a = load_group(kp, st, tb, e, min(m.u, U - 1), U, true);
+    GroupIn a = load_group<SCN>(kp, st, tb, e, min(m.u, U - 1), U, true);
     // per-env layouts: the env's station keys in the wave's LDS slots, 16 per env, as
     // {m = -16 q (int16x2), c = ((|q|^2 + 2^21) << 4) | j}, so that the key of station j for
     // a UE at p is ONE dot product: dot2(2 p, m) + c = ((|p - q|^2 - |p|^2 + 2^21) << 4) | j
@@ -1437,8 +1466,8 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
                           traj ? (uint32_t)(nsteps - 1) : 0u);
     // the state after the last step
     if (env_ok && m.u < U)
-      store_ue(&at(st.ue_state, 8u * (uint32_t)(e * U + m.u)), make_int2(a.s.x, a.s.y),
-               make_int2(a.s.z, a.s.w));
+      store_ue_at(st.ue_state, (uint32_t)(e * U + m.u), make_int2(a.s.x, a.s.y),
+                  make_int2(a.s.z, a.s.w), KST8);
     // the env's stream moved during the launch: some lane of it owned a new state
     const uint64_t mv = bal(moved);
     moved = ROWS ? seg_field<PC>(mv, m) != 0u : (mv & m.segmask) != 0;
@@ -1476,15 +1505,15 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
   return B + 1 > 64 / G ? B + 1 : 64 / G;
 }
-// A group's context in k_steps_lds2. The per-env flags are wave lane masks (every lane of an env
-// holds its env's bit), changed only inside the wave-uniform draw / reset branch: as per-lane
-// bools the compiler kept them as lane masks anyway and merged them across every divergent
-// region of the step (three s_andn2 / s_and / s_or per flag and group, every step).
-//   sok_w: the env's stream slot holds its stream state (draws past the episode draw table);
-//   mov_w: the env drew past the table in this pair (its state row is stored at the pair end).
+// A group's context in k_steps_lds2. The per-env flags are bits of one int per lane (the env's
+// value in each of its lanes), changed only inside the wave-uniform draw / reset branch: as
+// per-lane bools the compiler kept them as SGPR lane masks and merged them across every
+// divergent region of the step (three s_andn2 / s_and / s_or per flag and group, every step).
+//   bit 0 (kSok): the env's stream slot holds its stream state (draws past the episode table);
+//   bit 1 (kMov): the env drew past the table in this pair (its state row is stored at the end).
+constexpr int kSok = 1, kMov = 2;
 struct Ctx2 {
-  int t, drawn;
-  uint64_t sok_w, mov_w;
+  int t, drawn, fl;
   int2 pos, wp;
 };
 
@@ -1577,7 +1606,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
         fell_back = true;
         const u128 inc = slot[1];
         u128 s;
-        if (seg_field<PC>(c[r].sok_w, m) == 0u && c[r].drawn > 0) {
+        if (!(c[r].fl & kSok) && c[r].drawn > 0) {
           s = at(const_cast<u128*>(tb.tab_st),
                  16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(min(c[r].drawn, M) - 1)));
           wait_vmem();
@@ -1602,16 +1631,17 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     if (mneed_w[r] | rs_w[r]) {
       // the slot holds the state after draws past the table (fell_back, uniform); a draw from
       // the table or a reset leaves it to the table: per env, as lane masks (see Ctx2)
-      const uint64_t tw = bal(tot[r] > 0), zw = tw | rs_w[r];
+      const bool tw = tot[r] > 0;
+      int f = c[r].fl;
       if (fell_back) {
         const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
                              (do_reset[r] && tot[r] == 0 && u == U - 1);
         if (own_fin) slot[0] = s_fin;
-        c[r].sok_w = (c[r].sok_w & ~rs_w[r]) | tw;
-        c[r].mov_w |= tw;
+        f = tw ? (f | kSok | kMov) : reset_env[r] ? (f & ~kSok) : f;
       } else {
-        c[r].sok_w &= ~zw;
+        f = (tw || reset_env[r]) ? (f & ~kSok) : f;
       }
+      c[r].fl = f;
       c[r].drawn += tot[r];
     }
   }
@@ -1863,6 +1893,7 @@ __device__ uint64_t* g_mev_ts;
 template <int R, int NT, int NK>
 struct Pre2 {
   v2u32 s[R];   // the lane's UE row {x, y, wx, wy} (int16x4) in each group
+  int s8[R];    // the same in the compact form (uint8x4, KParams::st8)
   int t, d, c;  // lanes [0, R G): t, drawn and (per-env layouts) the station count of env slot
                 // `lane` (each from a wave-uniform base: no per-lane pointer kept live)
   v2u32 pc;     // lanes [0, 4 R G): word lane & 3 of {state, inc} of env slot lane >> 2
@@ -1902,11 +1933,14 @@ __device__ __forceinline__ void pf_tie(T& x) {
   asm volatile("; mev-prefetch-wait %0" : "+v"(x));
 }
 template <int R, int NT, int NK, bool PE>
-__device__ __forceinline__ void lds2_pf_wait(Pre2<R, NT, NK>& f, bool saturated) {
+__device__ __forceinline__ void lds2_pf_wait(Pre2<R, NT, NK>& f, bool saturated, bool st8) {
   if (saturated) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int r = 0; r < R; ++r) pf_tie(f.s[r]);
+  for (int r = 0; r < R; ++r) {
+    if (st8) pf_tie(f.s8[r]);
+    else pf_tie(f.s[r]);
+  }
   pf_tie(f.t);
   pf_tie(f.d);
   if (PE) pf_tie(f.c);
@@ -1919,7 +1953,7 @@ __device__ __forceinline__ void lds2_pf_wait(Pre2<R, NT, NK>& f, bool saturated)
   }
 }
 
-template <int UC, int SCN, int R, bool PE, int NT, int NK>
+template <int UC, int SCN, int R, bool PE, int NT, int NK, bool C8>
 __device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& st,
                                               const KTables& tb, const LaneMap& m, int lane,
                                               int p, Pre2<R, NT, NK>& f) {
@@ -1929,7 +1963,9 @@ __device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& s
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int ec = min(e0 + r * G + m.seg, elast);
-    f.s[r] = pf_b64(st.ue_state + (ec * U + min(m.u, U - 1)));
+    const uint32_t ui = (uint32_t)(ec * U + min(m.u, U - 1));
+    if (C8) f.s8[r] = pf_b32(reinterpret_cast<const unsigned*>(st.ue_state) + ui);
+    else f.s[r] = pf_b64(st.ue_state + ui);
   }
   const int ej = min(e0 + min(lane, RG - 1), elast);
   f.t = pf_b32(st.t + ej);
@@ -1953,7 +1989,7 @@ __device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& s
 
 // The prefetched inputs into the pair's contexts and the wave's LDS (draw tables, stream
 // slots, per-env station keys; t / drawn / counts through `scratch`, a free histogram area).
-template <int UC, int SCN, int R, bool PE, int NT, int NK>
+template <int UC, int SCN, int R, bool PE, int NT, int NK, bool C8>
 __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st, const LaneMap& m,
                                              int lane, int p, Pre2<R, NT, NK>& f, bool saturated,
                                              Ctx2 (&c)[R], int* __restrict__ ltab,
@@ -1961,7 +1997,7 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
                                              int* __restrict__ lkeys) {
   constexpr int PC = pitch_of(UC), G = 64 / PC, RG = R * G;
   const int M = KPS(tab_m);
-  lds2_pf_wait<R, NT, NK, PE>(f, saturated);
+  lds2_pf_wait<R, NT, NK, PE>(f, saturated, C8);
   const int lim = max(1, min(RG * M, (kp.E - p * RG) * M));
 #pragma unroll
   for (int q = 0; q < NT; ++q)
@@ -1997,11 +2033,16 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
     c[r].t = scratch[slot];
     c[r].drawn = scratch[RG + slot];
     // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
-    c[r].sok_w = bal(c[r].drawn > M);
-    c[r].mov_w = 0;
-    const int2 v = make_int2((int)f.s[r].x, (int)f.s[r].y);
-    c[r].pos = make_int2((int)(short)v.x, v.x >> 16);
-    c[r].wp = make_int2((int)(short)v.y, v.y >> 16);
+    c[r].fl = c[r].drawn > M ? kSok : 0;
+    if (C8) {
+      const int4 q = unpack8((unsigned)f.s8[r]);
+      c[r].pos = make_int2(q.x, q.y);
+      c[r].wp = make_int2(q.z, q.w);
+    } else {
+      const int2 v = make_int2((int)f.s[r].x, (int)f.s[r].y);
+      c[r].pos = make_int2((int)(short)v.x, v.x >> 16);
+      c[r].wp = make_int2((int)(short)v.y, v.y >> 16);
+    }
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -2019,7 +2060,9 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 // and rate_full over S; the env's station keys are staged per launch like k_steps_packed's)
 // R = 2 env groups per wavefront; R = 1 (batches too small to fill the resident workgroups
 // with pairs: one group per wavefront, the same step code).
-template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2>
+// C8: the compact UE state form (KParams::st8) as a compile-time property of the instance (the
+// prefetch registers of one form only: a runtime choice kept both sets live, and spilled them)
+template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2, bool C8 = scn_st8(SCN)>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -2059,12 +2102,12 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     const int n16 = KPS(lds_assoc) >> 4;
     for (int q = wv; q * 64 < n16; q += NW)
       if (q * 64 + lane < n16) glds(tb.lds_blob + q * 64 + lane, reinterpret_cast<int4*>(lds_all) + q * 64);
-    if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, PE, NT, NK>(kp, st, tb, m, lane, pb0 + wvu, f);
+    if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pb0 + wvu, f);
     wait_vmem();
     __syncthreads();
     MEV_TS(1);
     if (pb0 + wvu < npairs)
-      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pb0 + wvu, f, false, c, ltab, lpcg,
+      lds2_consume<UC, SCN, R, PE, NT, NK, C8>(kp, st, m, lane, pb0 + wvu, f, false, c, ltab, lpcg,
                                            hist, lkeys);
     MEV_TS(2);
   }
@@ -2082,13 +2125,13 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   int hb = 0;  // the pair's first row slot (alt)
   const bool leader = m.u == PC - 1;
   const int kval = m.u < U ? m.seg : 99, klead = m.u == PC - 1 ? m.seg : 99;
-  const uint32_t bst = 8u * (uint32_t)(kp.E * U), bt = 4u * (uint32_t)kp.E;
+  const uint32_t bst = (C8 ? 4u : 8u) * (uint32_t)(kp.E * U), bt = 4u * (uint32_t)kp.E;
   int it = 0;  // (MEV_TIMING)
   (void)it;
   for (int pb = pb0; pb < npairs; pb += gstride) {
     const int p = pb + wvu, pn = p + gstride;  // this wave's current / next pair
     const bool cur_ok = p < npairs, nxt_ok = pn < npairs;
-    if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK>(kp, st, tb, m, lane, pn, f);
+    if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pn, f);
     int* const sw = srow + hb * NWG;
     uint8_t* const dw = drow + hb * NWG;
     const int e0 = pb * G * R;  // the current tile's first env
@@ -2128,12 +2171,18 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       // global load here, whose wait would drain every store of the pair
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int2 pw = make_int2((int)(((unsigned)c[r].pos.x & 0xffffu) | ((unsigned)c[r].pos.y << 16)),
-                                  (int)(((unsigned)c[r].wp.x & 0xffffu) | ((unsigned)c[r].wp.y << 16)));
-        const v2u32 pv = {(unsigned)pw.x, (unsigned)pw.y};
-        __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
-                                              env_ok[r] && m.u < U ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
-        const bool mvd = seg_field<PC>(c[r].mov_w, m) != 0u;
+        const bool sv_ok = env_ok[r] && m.u < U;
+        if (C8) {
+          __builtin_amdgcn_raw_buffer_store_b32(pack8(c[r].pos, c[r].wp), out_rsrc(st.ue_state, bst),
+                                                sv_ok ? 4u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
+        } else {
+          const int2 pw = make_int2((int)(((unsigned)c[r].pos.x & 0xffffu) | ((unsigned)c[r].pos.y << 16)),
+                                    (int)(((unsigned)c[r].wp.x & 0xffffu) | ((unsigned)c[r].wp.y << 16)));
+          const v2u32 pv = {(unsigned)pw.x, (unsigned)pw.y};
+          __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
+                                                sv_ok ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
+        }
+        const bool mvd = (c[r].fl & kMov) != 0;
         const bool ld = env_ok[r] && leader;
         __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].t, out_rsrc(st.t, bt),
                                               ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
@@ -2143,12 +2192,12 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         const v4u32 sv = {(unsigned)(uint64_t)sl, (unsigned)((uint64_t)sl >> 32),
                           (unsigned)(uint64_t)(sl >> 64), (unsigned)((uint64_t)(sl >> 64) >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(sv, out_rsrc(st.pcg, 12u * bt),
-                                               ld && mvd && seg_field<PC>(c[r].sok_w, m) != 0u
+                                               ld && mvd && (c[r].fl & kSok)
                                                    ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
       }
     }
     if (nxt_ok) {  // the next pair's inputs (waited for: free after a whole pair's stores)
-      lds2_consume<UC, SCN, R, PE, NT, NK>(kp, st, m, lane, pn, f, saturated, c, ltab, lpcg, hist,
+      lds2_consume<UC, SCN, R, PE, NT, NK, C8>(kp, st, m, lane, pn, f, saturated, c, ltab, lpcg, hist,
                                            lkeys);
       MEV_TS(min(4 + 3 * it, 28));
     }
@@ -2189,7 +2238,7 @@ __global__ __launch_bounds__(1024) void k_reset_block(KParams kp, KState st, KOu
   u128 s_fin = s0;
   if (valid) s_fin = pcg_draw_pair(s0, mk128(b2.x, b2.y), 2 * u, tb.jump, kp.Wd, kp.Hd, x, y);
   if (valid) {
-    store_ue(st.ue_state + idx, make_int2(x, y), make_int2(-1, -1));
+    store_ue_at(st.ue_state, (uint32_t)idx, make_int2(x, y), make_int2(-1, -1), kp.st8 != 0);
     out.serving[idx] = -1;
     out.obs[idx] = make_float4((float)x * kp.inv_w, (float)y * kp.inv_h, 0.f, 0.f);
     if (out.rate64) out.rate64[idx] = 0.0;
@@ -2553,7 +2602,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       pos[h] = make_int2(0, 0);
       wp[h] = make_int2(-1, -1);
       if (valid[h]) {
-        const int4 sv = load_ue(st.ue_state + ebase + uh[h]);
+        const int4 sv = load_ue_at(st.ue_state, (uint32_t)(ebase + uh[h]), KST8);
         pos[h] = make_int2(sv.x, sv.y);
         wp[h] = make_int2(sv.z, sv.w);
       }
@@ -2972,7 +3021,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // ---- epilogue: the state after the last step ----------------------------------------
 #pragma unroll
     for (int h = 0; h < UPL; ++h)
-      if (valid[h]) store_ue(st.ue_state + ebase + uh[h], pos[h], wp[h]);
+      if (valid[h]) store_ue_at(st.ue_state, (uint32_t)(ebase + uh[h]), pos[h], wp[h], KST8);
     if (tid == 0) {
       st.t[e] = t;
       if (M) tb.drawn[e] = drawn;
@@ -3344,6 +3393,9 @@ const char* mev_strerror(int code) {
 static int validate(const mev_params* p) {
   if (!p) return MEV_EINVAL;
   if (p->num_envs < 1 || p->num_ues < 1 || p->num_ues > kMaxU) return MEV_EINVAL;
+  if (p->compact_state < 0 || p->compact_state > 1 ||
+      (p->compact_state && (p->width > 255 || p->height > 255)))
+    return MEV_EINVAL;
   if (p->num_bs < 1 || p->num_bs > kMaxB) return MEV_EINVAL;
   if (p->width < 1 || p->height < 1 || p->width > kMaxMap || p->height > kMaxMap) return MEV_EINVAL;
   if (p->ep_max_time < 1 || p->arrival_exit < 1) return MEV_EINVAL;
@@ -3420,7 +3472,7 @@ static int match_scn(const mev_ctx* ctx) {
   for (int s = 1; s <= 4; ++s) {
     const ScnConst c = scn_const(s);
     if ((s >= 3) != (ctx->p.bs_per_env != 0)) continue;
-    if ((s == 4) != (kp.U > 64) || kp.het) continue;
+    if ((s == 4) != (kp.U > 64) || kp.het || (kp.st8 != 0) != scn_st8(s)) continue;
     if (kp.U == c.U && kp.B == c.B && kp.W == c.W && kp.H == c.H && kp.tab_m == c.tab_m &&
         kp.hist_lds == c.hist_lds && kp.t_end == c.t_end && kp.arr_start == c.arr_start &&
         kp.arr_exit == c.arr_exit && kp.first_step_active == c.first_step_active &&
@@ -3876,6 +3928,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
   kp.xcd_remap = params->xcd_remap < 0 ? 0 : 1;
+  kp.st8 = params->compact_state;
   if (params->num_ues > 64 && params->station_culling >= 0) {  // block kernel (block_cull_params)
     const CullP cp = block_cull_params(params->num_bs, params->width, params->height,
                                        false);
@@ -4093,6 +4146,7 @@ int mev_step_shape(const mev_ctx* c) {
 }
 
 int mev_lds_tables_bytes(const mev_ctx* c) { return c ? c->kp.lds_assoc : MEV_EINVAL; }
+int mev_state_bytes_per_ue(const mev_ctx* c) { return c ? (c->kp.st8 ? 4 : 8) : MEV_EINVAL; }
 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 
@@ -4235,10 +4289,13 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     const bool pre_ok = 2 * kp.envs_per_wave * kp.tab_m <= 64 * lds2_pre_words<30, 0, 2>();
     if (c->p.bs_per_env && kp.lds_mode == 4 && lean && traj && c->lds2_wgs > 0 && pre_ok &&
         pairs >= c->lds2_wgs * kLds2Waves) {  // per-env layouts (k_steps_lds2<U, 0, true>)
-      StepsKernel k2 = kp.U == 15 ? k_steps_lds2<15, 0, true>
+      const bool c8 = kp.st8 != 0;  // (generic instances: the state form as a template flag)
+      StepsKernel k2 = kp.U == 15 ? (c8 ? k_steps_lds2<15, 0, true, false, 2, true>
+                                        : k_steps_lds2<15, 0, true>)
                                   : (match_scn(c) == 3 ? (c->tie_free ? k_steps_lds2<30, 3, true, true>
                                                                       : k_steps_lds2<30, 3, true>)
-                                                       : k_steps_lds2<30, 0, true>);
+                                     : c8 ? k_steps_lds2<30, 0, true, false, 2, true>
+                                          : k_steps_lds2<30, 0, true>);
       const int blocks = std::min((pairs + kLds2Waves - 1) / kLds2Waves, c->lds2_wgs);
       const int G = kp.envs_per_wave;
       const int srows = std::min(c->stage_rows2, nsteps);
@@ -4266,17 +4323,22 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
       StepsKernel k2;
+      const bool c8 = kp.st8 != 0;  // (generic instances: the state form as a template flag)
       if (R == 2)
         k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true> : k_steps_lds2<15, 1>)
+                           : c8     ? k_steps_lds2<15, 0, false, false, 2, true>
                                     : k_steps_lds2<15, 0>)
                         : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true> : k_steps_lds2<30, 2>)
+                           : c8     ? k_steps_lds2<30, 0, false, false, 2, true>
                                     : k_steps_lds2<30, 0>);
       else
         k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true, 1>
                                           : k_steps_lds2<15, 1, false, false, 1>)
+                           : c8     ? k_steps_lds2<15, 0, false, false, 1, true>
                                     : k_steps_lds2<15, 0, false, false, 1>)
                         : (scn == 2 ? (tf ? k_steps_lds2<30, 2, false, true, 1>
                                           : k_steps_lds2<30, 2, false, false, 1>)
+                           : c8     ? k_steps_lds2<30, 0, false, false, 1, true>
                                     : k_steps_lds2<30, 0, false, false, 1>);
       const int blocks = std::min((units + nw2 - 1) / nw2, c->lds2_wgs);
       const int G = kp.envs_per_wave;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -22,7 +22,7 @@ MEV_EHIP = -1000
 MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
-EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes",
+EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes", "mev_state_bytes_per_ue",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations", "mev_update_layouts", "mev_build_rate_table", "mev_share_cents",
            "mev_rollout_instance", "mev_share_tie_free",
@@ -54,6 +54,7 @@ class MevParams(C.Structure):
         ("station_culling", C.c_int32),
         ("ues_per_lane", C.c_int32),
         ("ue_velocity", C.c_void_p),
+        ("compact_state", C.c_int32),
     ]
 
 
@@ -105,6 +106,8 @@ def lib():
         L.mev_step_shape.restype = C.c_int
         L.mev_lds_tables_bytes.argtypes = [C.c_void_p]
         L.mev_lds_tables_bytes.restype = C.c_int
+        L.mev_state_bytes_per_ue.argtypes = [C.c_void_p]
+        L.mev_state_bytes_per_ue.restype = C.c_int
         L.mev_rate_table.argtypes = [C.c_void_p]
         L.mev_rate_table.restype = C.c_void_p
         L.mev_copy_rate_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]

@@ -73,6 +73,15 @@ class EngineParams:
     # per-UE velocity (mev_params.ue_velocity; None: `velocity` / the UE's class's): velocity
     # drives only the movement, so any number of distinct values needs no class
     ue_velocity: "list | None" = None  # [U]
+    # UE state form (mev_params.compact_state): 0 auto -- uint8 x4 per UE on maps <= 255 per
+    # side (every registered scenario), else int16 x4; -1 always int16; 1 uint8 (maps <= 255)
+    compact_state: int = 0
+
+    @property
+    def state_u8(self) -> bool:
+        if self.compact_state < 0:
+            return False
+        return self.compact_state > 0 or (int(self.width) <= 255 and int(self.height) <= 255)
 
     @property
     def heterogeneous(self) -> bool:
@@ -151,6 +160,7 @@ class EngineParams:
             stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
             scenario_constants=int(self.scenario_constants),
             station_culling=int(self.station_culling), ues_per_lane=int(self.ues_per_lane),
+            compact_state=int(self.state_u8),
             ue_velocity=(arr([float(v) for v in self.ue_velocity], np.float64)
                          if self.ue_velocity is not None else C.c_void_p(None)))
         cp._keep = keep
@@ -249,7 +259,10 @@ class StepEngine:
                 self.bs_count = torch.as_tensor(bs_count, dtype=torch.int32).reshape(E).to(**kw)
                 if int(self.bs_count.max()) > B or int(self.bs_count.min()) < 0:
                     raise ValueError("bs_count out of range")
-            self.ue_state = torch.full((E, U, 4), -1, dtype=torch.int16, **kw)
+            # the kernels' UE state rows: uint8 x4 (compact form, 255 = -1) or int16 x4
+            self._u8 = params.state_u8
+            self._ue_raw = torch.full((E, U, 4), 255 if self._u8 else -1,
+                                      dtype=torch.uint8 if self._u8 else torch.int16, **kw)
             self.t = torch.full((E,), params.t_end, dtype=torch.int32, **kw)
             self._pcg = torch.zeros((E, 6), dtype=torch.int64, **kw)
             self.obs = torch.zeros((E, U, 4), dtype=torch.float32, **kw)
@@ -271,7 +284,7 @@ class StepEngine:
 
     # -- plumbing -----------------------------------------------------------------------------
     def _bind(self):
-        self._st = N.MevState(_ptr(self.ue_state), _ptr(self._pcg), _ptr(self.t),
+        self._st = N.MevState(_ptr(self._ue_raw), _ptr(self._pcg), _ptr(self.t),
                               _ptr(self.bs_xy), _ptr(self.bs_count))
         self._out = N.MevOutputs(_ptr(self.obs), _ptr(self.serving), _ptr(self.reward),
                                  _ptr(self.done), _ptr(self.rate64), _ptr(self.util64),
@@ -281,13 +294,28 @@ class StepEngine:
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     @property
+    def ue_state(self):
+        """UE state rows [E,U,4] int16 {x, y, wx, wy} (wx < 0: no waypoint): the kernels' rows
+        (mev_state.ue_state) in their int16 form -- a decoded copy where the context keeps the
+        compact uint8 form (255 = -1; maps <= 255 per side). Write rows with restore_state."""
+        if not self._u8:
+            return self._ue_raw
+        v = self._ue_raw.to(torch.int16)
+        return torch.where(v == 255, torch.full_like(v, -1), v)
+
+    @property
+    def state_bytes_per_ue(self) -> int:
+        """4 (compact uint8 x4 rows) or 8 (int16 x4) -- mev_state_bytes_per_ue."""
+        return int(self._lib.mev_state_bytes_per_ue(self._ctx))
+
+    @property
     def ue_xy(self):
-        """UE positions [E,U,2] (view of ue_state)."""
-        return self.ue_state[..., :2]
+        """UE positions [E,U,2] (int16; a view of the rows in the int16 form)."""
+        return self._ue_raw[..., :2] if not self._u8 else self._ue_raw[..., :2].to(torch.int16)
 
     @property
     def wp_xy(self):
-        """RandomWaypoint targets [E,U,2] (view of ue_state; x < 0: none)."""
+        """RandomWaypoint targets [E,U,2] (int16; x < 0: none)."""
         return self.ue_state[..., 2:]
 
     @property
@@ -386,7 +414,7 @@ class StepEngine:
         self.sync_stream_state()
         return self._pcg
 
-    def restore_state(self, ue_state, pcg, t, mask=None):
+    def restore_state(self, ue_state, pcg, t, mask=None, declare=True):
         """Load a checkpoint {ue_state [E,U,4] int16, pcg [E,6] (as read from ``pcg``), t [E]}
         taken at any step of an episode (all envs, or those with mask[e]) and continue from it:
         the envs' waypoint draws continue from the saved stream states until their next reset
@@ -395,13 +423,18 @@ class StepEngine:
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.bool)
         src = [torch.as_tensor(x, device=self.device) for x in (ue_state, pcg, t)]
-        for dst, x in zip((self.ue_state, self._pcg, self.t), src):
+        if self._u8:  # the compact form: -1 -> 255
+            v = src[0].to(torch.int16)
+            src[0] = torch.where(v < 0, torch.full_like(v, 255), v)
+        for dst, x in zip((self._ue_raw, self._pcg, self.t), src):
             x = x.to(dst.dtype).reshape(dst.shape)
             if m is None:
                 dst.copy_(x)
             else:
                 dst[m] = x[m]
         mk = m.to(torch.uint8).contiguous() if m is not None else None
+        if not declare:  # (tests: the rows alone, as a caller forgetting the call would)
+            return
         with torch.cuda.device(self.device):
             N.check(self._lib.mev_restore_stream_state(self._ctx, C.byref(self._st), _ptr(mk),
                                                        self._stream()),

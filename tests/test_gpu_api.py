@@ -238,9 +238,7 @@ def test_checkpoint_restore_mid_episode(U, B, launch):
     a.step(7)
     ck = (a.ue_state.clone(), a.pcg.clone(), a.t.clone())
     b.restore_state(*ck)
-    c.ue_state.copy_(ck[0])  # the same rows without the restore call (the bug's shape)
-    c._pcg.copy_(ck[1])
-    c.t.copy_(ck[2])
+    c.restore_state(*ck, declare=False)  # the same rows without the restore call (the bug)
     n = 33  # the rest of episode 1 (13 steps) and one more episode
 
     def run(eng):

@@ -109,4 +109,20 @@ for n in LENS:
                       "iso_us_per_step": statistics.median(iso_ev) * 1e3 / n,
                       "env_steps_per_s_iso_wall": E * n / (statistics.median(iso_wall) * 1e-3)}),
           flush=True)
+if os.environ.get("SINGLE"):  # one-step launches (make().step(), mev_step(1)), back to back
+    go1 = eng.launcher(1)
+    for _ in range(50):
+        go1()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(100):
+            go1()
+        b.record(stream)
+        torch.cuda.synchronize()
+        res.append(a.elapsed_time(b) * 10.0)  # us per launch
+    print(json.dumps({"n": 1, "engine": over, "single_us_median": statistics.median(res),
+                      "single_us_min": min(res)}), flush=True)
 env.close()
