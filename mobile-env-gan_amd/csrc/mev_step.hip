@@ -544,6 +544,23 @@ __device__ __forceinline__ int seg_isum_rows(int x) {
   return x;
 }
 
+// ResourceFair's n_b without LDS for 16-lane segments (P = 16: one DPP row per env) with at
+// most 15 UEs and 8 stations: every lane adds 1 << 4 srv into a row-wide sum (butterfly over
+// row_ror 8 / 4 / 2 / 1: the total in every lane of the row), i.e. 8 packed 4-bit counts, and
+// reads its own station's field. No LDS round trips (zero, atomic add, read back) on the step's
+// dependency chain -- which is what bounds a wave alone on its SIMD (small batches).
+__host__ __device__ constexpr bool packed_counts_ok(int UC, int B) {
+  return UC >= 1 && UC <= 15 && B >= 1 && B <= 8;
+}
+__device__ __forceinline__ int row_count_same(int srv) {
+  int v = srv >= 0 ? 1 << (4 * srv) : 0;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x122, 0xf, 0xf, false);  // row_ror:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x121, 0xf, 0xf, false);  // row_ror:1
+  return srv >= 0 ? (int)__builtin_amdgcn_ubfe((uint32_t)v, (uint32_t)(4 * srv), 4u) : 0;
+}
+
 // Float32 form of the scaled BoundedLogUtility (used when no float64 utility output is
 // requested): clip(w1 log(w2 + r) / log(w3), lower, upper) with log via v_log_f32, then the
 // affine scale to [-1, 1]; r = (float)cents * 0.01f is the obs rate. Relative error ~1e-7 of
@@ -1089,7 +1106,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // ---- 3. n_b of the own serving BS ---------------------------------------------------
   const uint64_t mcon = bal(srv >= 0) & segmask;
   int n;
-  if (KPS(hist_lds)) {
+  if (PC == 16 && SCN && packed_counts_ok(UC, KPS(B))) {
+    n = row_count_same(srv);  // (registered scenarios: B is a compile-time constant)
+  } else if (KPS(hist_lds)) {
     // per-env histogram in the wavefront's own LDS slice [G][B]: zero, count, read back
     // (one wavefront's LDS instructions execute in order: no barrier)
     int* h = hist + m.seg * KPS(B);
@@ -1750,24 +1769,32 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     }
   }
   // per-env histograms in the wave's LDS (bin B: lanes without a station): zero, count, read
+  // (16-lane segments of a registered scenario: packed DPP counts instead, row_count_same)
+  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(UC, SCN ? scn_const(SCN).B : 0);
   int* h[R];
   int bin[R], n[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     h[r] = hist + (r * G + m.seg) * HS;
     bin[r] = srv[r] >= 0 ? srv[r] : B;
-    h[r][HS >= PC ? u : min(u, B)] = 0;  // (u < PC: one word per lane)
+    if (!PCNT) h[r][HS >= PC ? u : min(u, B)] = 0;  // (u < PC: one word per lane)
   }
-  __builtin_amdgcn_wave_barrier();
+  if (PCNT) {
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-    __hip_atomic_fetch_add(h[r] + bin[r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-  __builtin_amdgcn_wave_barrier();
+    for (int r = 0; r < R; ++r) n[r] = row_count_same(srv[r]);
+  } else {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      __hip_atomic_fetch_add(h[r] + bin[r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) n[r] = min(h[r][bin[r]], 64);
+  }
   float cf[R];
   bool tie[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    n[r] = min(h[r][bin[r]], 64);
     const double r100 = *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n[r]);
     // share_cents_r (ResourceFair share + numpy round(., 2)), the tie test in float32
     const double cc = full[r] * r100;
@@ -2637,7 +2664,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int tlim = M;
     if (M && !tab_g)
       for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tab_src[k];
-    auto tab_at = [&](int k) { return tab_g ? tab_src[k] : L.tab[k - tb0]; };  // (k < M)
+    // (k < M; a buffer load for the HBM table and an LDS read otherwise, as a uniform branch: a
+    // select between the two pointers made the compiler emit flat loads, which wait on both
+    // counters, and keep a 64-bit address live across the step)
+    const __amdgpu_buffer_rsrc_t tab_rs = out_rsrc(tab_src, 4u * (uint32_t)M);
+    auto tab_at = [&](int k) -> int {
+      if (tab_g) return (int)__builtin_amdgcn_raw_buffer_load_b32(tab_rs, 4u * (uint32_t)k, 0, 0);
+      return L.tab[k - tb0];
+    };
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     const bool wide = KPS(W) > 1024 || KPS(H) > 1024;  // (uniform; a scenario: constant false)
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
@@ -2695,6 +2729,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const bool wcell = pers || UPL == 2;
     const int RLOG = wcell ? pc.log : CLOG, RNX = wcell ? pc.nx : CNX, RNC = wcell ? pc.nc : CNC;
     const unsigned char* const grec = pers ? tb.crec_g + (size_t)erec * pc.nc * 16 : nullptr;
+    const __amdgpu_buffer_rsrc_t grec_rs = out_rsrc(grec, pers ? 16u * (uint32_t)pc.nc : 0u);
     if (cull && !pers) {
       cull_cells(lds_keys, nb, RLOG, RNX, RNC, KPS(W), KPS(H), tid, nt, crec);
       __syncthreads();
@@ -2852,8 +2887,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         for (int h = 0; h < UPL; ++h) {
           const int cell = min(__mul24(max(pos[h].y, 0) >> RLOG, RNX) + (max(pos[h].x, 0) >> RLOG),
                                RNC - 1);
-          rec[h] = pers ? *reinterpret_cast<const v4u32*>(grec + 16 * cell)
-                        : *reinterpret_cast<const v4u32*>(crec + 16 * cell);
+          // (a uniform branch: a select between the HBM and LDS pointers became flat loads)
+          if (pers)
+            rec[h] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   grec_rs, 16u * (uint32_t)cell, 0, 0));
+          else
+            rec[h] = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
         }
 #pragma unroll
         for (int h = 0; h < UPL; ++h) {

