@@ -1858,7 +1858,8 @@ __device__ __forceinline__ void lds_barrier() {
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
-__device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
+__device__ __forceinline__ __attribute__((unused)) void flush_staged2(
+    const KOut& out, const int* srow, const uint8_t* drow,
                                               int E, int e0, int row0, int nr, float lower,
                                               int NWG, bool trailing = true) {
   lds_barrier();
@@ -1875,6 +1876,36 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
     }
   }
   if (trailing) lds_barrier();
+}
+
+// The staged rows of ONE wave's envs (RG of them, contiguous: the wave's pair), written by the
+// wave itself when its window is full or its pair ends: rows r0 .. r0 + nr - 1 of the window go
+// to trajectory rows row0 .. row0 + nr - 1. No workgroup barrier: with the tile-wide flush
+// (flush_staged2, -DMEV_LDS2_WGFLUSH) every pair ended in a barrier of the workgroup's 16 waves,
+// each paying the drift between them. sw / dw: the wave's entries of window row 0 (row stride
+// NWG); one wave's LDS operations complete in order, so its staged writes precede these reads.
+template <int RG>
+__device__ __forceinline__ void flush_wave(const KOut& out, const int* sw, const uint8_t* dw,
+                                           int NWG, int E, int e0, int row0, int r0, int nr,
+                                           float lower, int lane) {
+  asm volatile("" ::: "memory");
+  // buffer stores from the first row's base (scalar 64-bit math only; lanes past the batch's
+  // last env store out of range, which the range check drops)
+  const uint32_t nb = (uint32_t)nr * (uint32_t)E;
+  const __amdgpu_buffer_rsrc_t rrs = out_rsrc(out.reward + (size_t)row0 * (size_t)E, 4u * nb);
+  const __amdgpu_buffer_rsrc_t drs = out_rsrc(out.done + (size_t)row0 * (size_t)E, nb);
+  for (int q = lane; q < nr * RG; q += 64) {
+    const int r = q / RG, j = q - r * RG;
+    const int off = (r0 + r) * NWG + j;
+    const int sv = sw[off];
+    const uint32_t b = dw[off];
+    const int nact = (int)(b & 0x7fu);
+    const float rew = nact > 0 ? (float)sv * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
+    const uint32_t o = e0 + j < E ? (uint32_t)r * (uint32_t)E + (uint32_t)(e0 + j) : nb;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rew), rrs, 4u * o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(b >> 7), drs, o, 0, 0);
+  }
+  asm volatile("" ::: "memory");
 }
 
 // Dev builds only (-DMEV_TIMING, tools/ts_probe.py): per-wave timestamps of k_steps_lds2's
@@ -2147,7 +2178,11 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   // below -- so that 2R nsteps + 4R >= 64 of them make the wait free (vmcnt(63)).
   // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
   // halves (one barrier per flush), else the window cycles (two).
+#ifdef MEV_LDS2_WGFLUSH
   const bool alt = 2 * nsteps <= stage_rows;
+#else
+  const bool alt = false;  // (per-wave flushes: the window simply cycles)
+#endif
   const bool saturated = 2 * R * nsteps + 4 * R >= 64;  // (2R trajectory stores per step, 4R state)
   int hb = 0;  // the pair's first row slot (alt)
   const bool leader = m.u == PC - 1;
@@ -2161,7 +2196,9 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pn, f);
     int* const sw = srow + hb * NWG;
     uint8_t* const dw = drow + hb * NWG;
+#ifdef MEV_LDS2_WGFLUSH
     const int e0 = pb * G * R;  // the current tile's first env
+#endif
     if (cur_ok) {
       int e[R], nok[R];
       bool env_ok[R];
@@ -2180,8 +2217,14 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
               sw + sr * NWG + wvu * G * R, dw + sr * NWG + wvu * G * R, lkeys);
+#ifdef MEV_LDS2_WGFLUSH
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
             flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+#else
+          if (sr + 1 == stage_rows || i + 1 == nsteps)  // (outputs overwritten: the last row only)
+            flush_wave<G * R>(out, sw + wvu * G * R, dw + wvu * G * R, NWG, kp.E, p * G * R,
+                              traj ? i - sr : 0, traj ? 0 : sr, traj ? sr + 1 : 1, lower, lane);
+#endif
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         } while (i < nsteps);
@@ -2228,6 +2271,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
                                            lkeys);
       MEV_TS(min(4 + 3 * it, 28));
     }
+#ifdef MEV_LDS2_WGFLUSH
     if (alt) {
       flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
     } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
@@ -2235,6 +2279,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
                       NWG, true);
     }
+#endif
     MEV_TS(min(5 + 3 * it, 29));
     hb = alt ? nsteps - hb : 0;
     ++it;

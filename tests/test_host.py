@@ -350,6 +350,18 @@ def test_prefetch_registers_check_on_generated_assembly():
             "\tv_add_u32_e32 v7, v8, v6\n\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v5\n"
             "\tds_write_b32 v1, v5\n")
     assert cp.violations(good) == ([], 1)
+    # a 64-bit multiply-add that reads an in-flight register only as its addend's don't-care high
+    # half (the result's high half dead: redefined, after an unconditional branch, before any
+    # read) is benign; with the high half read afterwards, or a conditional branch first, not
+    head = ("_Zk:\n\tglobal_load_dword v43, v[2:3], off ; mev-prefetch\n"
+            "\tv_mad_u64_u32 v[0:1], s[8:9], s35, v7, v[42:43]\n")
+    tail = "\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v43\n"
+    dead = head + "\ts_branch .LBB0_2\n.LBB0_2:\n\tds_read_u8 v1, v0\n" + tail
+    assert cp.violations(dead) == ([], 1)
+    used = head + "\tv_add_u32_e32 v4, v1, v0\n" + tail
+    assert cp.violations(used)[0]
+    cond = head + "\ts_cbranch_scc1 .LBB0_2\n\tds_read_u8 v1, v0\n.LBB0_2:\n" + tail
+    assert cp.violations(cond)[0]
     text = open(cp.build_asm()).read()
     v, n = cp.violations(text)
     assert n >= 8 and v == []
