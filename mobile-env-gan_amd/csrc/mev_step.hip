@@ -170,6 +170,10 @@ struct KTables {
   // 0xF000 = no station in reach, 0xFFFF = k beyond 4094 (such cells take the L2 map);
   // [lds_r100_off, +576) 100 / n; [lds_rate_off, +32 KB) rate_full[d] for d in D, in increasing d.
   const int4* lds_blob;
+  // mode 3: |D|, the rates over D in use (k_d2_prefix, per layout): the copies into LDS stop
+  // at lds_rate_off + 8 |D| instead of the 4,096 rate slots reserved (113 -> 88 KB for
+  // mobile-large); null for the other modes
+  const int* dcount;
   // heterogeneous entities (KParams::het): per station class cb / UE class cu
   const uint8_t* bs_cls;    // [B] class of station j
   const uint8_t* ue_cls;    // [U] class of UE u
@@ -1286,6 +1290,15 @@ __device__ __forceinline__ int block_slot(int remap) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// 16-byte pieces of the LDS blob a rollout copies: all of it, or (mode 3) up to the rates over D
+// in use (KTables::dcount)
+template <int SCN>
+__device__ __forceinline__ int blob_copy_n16(const KParams& kp, const KTables& tb) {
+  const int all = KPS(lds_assoc) >> 4;
+  if (!tb.dcount) return all;
+  return min(all, (KPS(lds_rate_off) + 8 * *tb.dcount + 15) >> 4);
+}
+
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
 // Groups [g0, ngroups) of the batch (g0 > 0: second half of the two-stream shape).
 template <bool PER_ENV_BS, bool LEAN, int UC, int SCN = 0>
@@ -1369,7 +1382,7 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
   const char* lblob = nullptr;
   if (LDSA) {
     // LDS-DMA copy (no registers): wave w moves 1 KB pieces w, w + NW, ...
-    const int n16 = KPS(lds_assoc) >> 4;
+    const int n16 = blob_copy_n16<SCN>(kp, tb);
     const int ln = threadIdx.x & 63;
     for (int c = (int)(threadIdx.x >> 6); c * 64 < n16; c += NW)
       if (c * 64 + ln < n16) glds(tb.lds_blob + c * 64 + ln, reinterpret_cast<int4*>(lds_all) + c * 64);
@@ -2157,7 +2170,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   {  // the tables (LDS-DMA, wave w moves 1 KB pieces w, w + NW, ...) and the first pair's
      // inputs, issued together before one wait (before the pair loop: a wait inside it would
      // leave the compiler unsure the copy is done, and it would wait before LDS accesses)
-    const int n16 = KPS(lds_assoc) >> 4;
+    const int n16 = blob_copy_n16<SCN>(kp, tb);
     for (int q = wv; q * 64 < n16; q += NW)
       if (q * 64 + lane < n16) glds(tb.lds_blob + q * 64 + lane, reinterpret_cast<int4*>(lds_all) + q * 64);
     if (pb0 + wvu < npairs) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pb0 + wvu, f);
@@ -3306,6 +3319,7 @@ __global__ __launch_bounds__(1024) void k_d2_prefix(const uint8_t* __restrict__ 
     words[w].y = run;
     run += (uint32_t)__popc(words[w].x);
   }
+  if (t == 1023) words[nwords] = make_uint2(part[t], 0u);  // |D|: the rates a copy needs
 }
 
 constexpr uint32_t kLds3Rates = 4096;  // rate slots of a mode-3 blob (ranks 0..4094 used)
@@ -3683,7 +3697,7 @@ static int build_lds_tables(mev_ctx* c) {
     total = up16(rate_off + 8 * (size_t)kLds3Rates);
     if (total + kLds2Waves * (lds_per_wave(kp) + stage_bytes_per_row(kp)) + 4 <=
         (size_t)kLds2BytesPerWG) {
-      if (hipMalloc(&c->dwords, 8 * nwords) != hipSuccess) return MEV_ENOMEM;
+      if (hipMalloc(&c->dwords, 8 * (nwords + 1)) != hipSuccess) return MEV_ENOMEM;
       if (hipMalloc(&c->dflag, (size_t)d2max + 1) != hipSuccess) return MEV_ENOMEM;
       mode = 3;
     }
@@ -3942,6 +3956,8 @@ static KTables tables_of(const mev_ctx* c) {
   tb.tab_st = c->tab_st;
   tb.drawn = c->drawn;
   tb.lds_blob = c->blob;
+  tb.dcount = (c->blob && c->kp.lds_mode == 3 && c->dwords)
+                  ? reinterpret_cast<const int*>(c->dwords + c->nwords) : nullptr;
   tb.bs_cls = c->h_bcl;
   tb.ue_cls = c->h_ucl;
   tb.pair = c->h_pair;
