@@ -501,8 +501,12 @@ def main():
     # each launch: isolated launches when the region was one launch (the driver's shape), else
     # back to back like the region's
     reps = max(3, min(30, int(0.05 / max(CHUNK * 8e-6, 1e-6))))
-    chunk_ms, chunk_ms_med = launch_timing(issue, CHUNK, reps, sync, _WallEv if stub else _Ev,
-                                           isolated=len(plan) == 1)
+    if args.profile_run:  # (rocprofv3 runs: the timed region's launches stay the trace's last)
+        reps = 0
+        chunk_ms = chunk_ms_med = elapsed * 1e3 / len(plan)
+    else:
+        chunk_ms, chunk_ms_med = launch_timing(issue, CHUNK, reps, sync,
+                                               _WallEv if stub else _Ev, isolated=len(plan) == 1)
 
     step_roof = None
     if rank == 0 and fused and not args.profile_run and args.step_launches > 0 and not stub:
