@@ -323,6 +323,9 @@ def main():
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="engine launch-shape override (EngineParams: lds_tables, two_groups, "
                          "stage_rows, xcd_remap, scenario_constants), for A/B runs")
+    ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "block"),
+                    help="HIP host wait policy for synchronize (hipSetDeviceFlags before the "
+                         "device is initialised): auto (HIP's default), spin, blocking")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no step roofline)")
@@ -353,6 +356,12 @@ def main():
     else:
         ndev = max(1, torch.cuda.device_count())
         device = torch.device("cuda", local_rank % ndev)
+        if args.host_wait != "auto":  # before anything creates the device's context
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            assert hip.hipSetDevice(ctypes.c_int(device.index)) == 0
+            flag = {"spin": 1, "block": 4}[args.host_wait]  # hipDeviceSchedule{Spin,BlockingSync}
+            assert hip.hipSetDeviceFlags(ctypes.c_uint(flag)) == 0
         torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -577,6 +586,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": DTYPE,
+            "host_wait": args.host_wait,
             "data": "synthetic (seeded PCG64 streams, build-defined BS layout)",
             "config": {"workload": args.workload, "envs_per_gpu": E, "global_envs": world * E,
                        "num_ues": U, "num_bs": B, "per_env_layouts": bool(per_env_bs),
