@@ -142,7 +142,8 @@ typedef struct mev_params {
    *     batch fills the GPU with pairs); 1 / 2: the two-group kernel with two / one groups
    *     per wavefront at any batch size;
    *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
-   *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges);
+   *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges; 2..8: the
+   *     ranges rotated by xcd_remap - 1 XCDs, a placement experiment);
    *   scenario_constants: -1: the generic kernel instances only (else a registered scenario's
    *     parameters are compiled in when every value matches);
    *   station_culling: -1: the U > 64 kernel scans every station per UE (else per-cell

@@ -1286,7 +1286,7 @@ __device__ __forceinline__ int block_slot(int remap) {
   const int orig = blockIdx.x;
   if (!remap) return orig;
   const int nwg = gridDim.x;
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int xcd = (orig + remap - 1) & 7, q = nwg >> 3, r = nwg & 7;  // (remap > 1: rotated, dev)
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
@@ -1871,8 +1871,7 @@ __device__ __forceinline__ void lds_barrier() {
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
-__device__ __forceinline__ __attribute__((unused)) void flush_staged2(
-    const KOut& out, const int* srow, const uint8_t* drow,
+__device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
                                               int E, int e0, int row0, int nr, float lower,
                                               int NWG, bool trailing = true) {
   lds_barrier();
@@ -1889,36 +1888,6 @@ __device__ __forceinline__ __attribute__((unused)) void flush_staged2(
     }
   }
   if (trailing) lds_barrier();
-}
-
-// The staged rows of ONE wave's envs (RG of them, contiguous: the wave's pair), written by the
-// wave itself when its window is full or its pair ends: rows r0 .. r0 + nr - 1 of the window go
-// to trajectory rows row0 .. row0 + nr - 1. No workgroup barrier: with the tile-wide flush
-// (flush_staged2, -DMEV_LDS2_WGFLUSH) every pair ended in a barrier of the workgroup's 16 waves,
-// each paying the drift between them. sw / dw: the wave's entries of window row 0 (row stride
-// NWG); one wave's LDS operations complete in order, so its staged writes precede these reads.
-template <int RG>
-__device__ __forceinline__ void flush_wave(const KOut& out, const int* sw, const uint8_t* dw,
-                                           int NWG, int E, int e0, int row0, int r0, int nr,
-                                           float lower, int lane) {
-  asm volatile("" ::: "memory");
-  // buffer stores from the first row's base (scalar 64-bit math only; lanes past the batch's
-  // last env store out of range, which the range check drops)
-  const uint32_t nb = (uint32_t)nr * (uint32_t)E;
-  const __amdgpu_buffer_rsrc_t rrs = out_rsrc(out.reward + (size_t)row0 * (size_t)E, 4u * nb);
-  const __amdgpu_buffer_rsrc_t drs = out_rsrc(out.done + (size_t)row0 * (size_t)E, nb);
-  for (int q = lane; q < nr * RG; q += 64) {
-    const int r = q / RG, j = q - r * RG;
-    const int off = (r0 + r) * NWG + j;
-    const int sv = sw[off];
-    const uint32_t b = dw[off];
-    const int nact = (int)(b & 0x7fu);
-    const float rew = nact > 0 ? (float)sv * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
-    const uint32_t o = e0 + j < E ? (uint32_t)r * (uint32_t)E + (uint32_t)(e0 + j) : nb;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rew), rrs, 4u * o, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(b >> 7), drs, o, 0, 0);
-  }
-  asm volatile("" ::: "memory");
 }
 
 // Dev builds only (-DMEV_TIMING, tools/ts_probe.py): per-wave timestamps of k_steps_lds2's
@@ -2191,11 +2160,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   // below -- so that 2R nsteps + 4R >= 64 of them make the wait free (vmcnt(63)).
   // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
   // halves (one barrier per flush), else the window cycles (two).
-#ifdef MEV_LDS2_WGFLUSH
   const bool alt = 2 * nsteps <= stage_rows;
-#else
-  const bool alt = false;  // (per-wave flushes: the window simply cycles)
-#endif
   const bool saturated = 2 * R * nsteps + 4 * R >= 64;  // (2R trajectory stores per step, 4R state)
   int hb = 0;  // the pair's first row slot (alt)
   const bool leader = m.u == PC - 1;
@@ -2209,9 +2174,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pn, f);
     int* const sw = srow + hb * NWG;
     uint8_t* const dw = drow + hb * NWG;
-#ifdef MEV_LDS2_WGFLUSH
     const int e0 = pb * G * R;  // the current tile's first env
-#endif
     if (cur_ok) {
       int e[R], nok[R];
       bool env_ok[R];
@@ -2230,14 +2193,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
               sw + sr * NWG + wvu * G * R, dw + sr * NWG + wvu * G * R, lkeys);
-#ifdef MEV_LDS2_WGFLUSH
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
             flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
-#else
-          if (sr + 1 == stage_rows || i + 1 == nsteps)  // (outputs overwritten: the last row only)
-            flush_wave<G * R>(out, sw + wvu * G * R, dw + wvu * G * R, NWG, kp.E, p * G * R,
-                              traj ? i - sr : 0, traj ? 0 : sr, traj ? sr + 1 : 1, lower, lane);
-#endif
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         } while (i < nsteps);
@@ -2284,7 +2241,6 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
                                            lkeys);
       MEV_TS(min(4 + 3 * it, 28));
     }
-#ifdef MEV_LDS2_WGFLUSH
     if (alt) {
       flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
     } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
@@ -2292,7 +2248,6 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
                       NWG, true);
     }
-#endif
     MEV_TS(min(5 + 3 * it, 29));
     hb = alt ? nsteps - hb : 0;
     ++it;
@@ -2722,14 +2677,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int tlim = M;
     if (M && !tab_g)
       for (int k = tb0 + tid; k < tlim; k += nt) L.tab[k - tb0] = tab_src[k];
-    // (k < M; a buffer load for the HBM table and an LDS read otherwise, as a uniform branch: a
-    // select between the two pointers made the compiler emit flat loads, which wait on both
-    // counters, and keep a 64-bit address live across the step)
-    const __amdgpu_buffer_rsrc_t tab_rs = out_rsrc(tab_src, 4u * (uint32_t)M);
-    auto tab_at = [&](int k) -> int {
-      if (tab_g) return (int)__builtin_amdgcn_raw_buffer_load_b32(tab_rs, 4u * (uint32_t)k, 0, 0);
-      return L.tab[k - tb0];
-    };
+    auto tab_at = [&](int k) { return tab_g ? tab_src[k] : L.tab[k - tb0]; };  // (k < M)
     const bool scaled = __syncthreads_and(in512) && KPS(W) <= 512 && KPS(H) <= 512;
     const bool wide = KPS(W) > 1024 || KPS(H) > 1024;  // (uniform; a scenario: constant false)
     // key slots: station k (homogeneous), or station perm[k] grouped by class (HET; padding
@@ -2787,7 +2735,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const bool wcell = pers || UPL == 2;
     const int RLOG = wcell ? pc.log : CLOG, RNX = wcell ? pc.nx : CNX, RNC = wcell ? pc.nc : CNC;
     const unsigned char* const grec = pers ? tb.crec_g + (size_t)erec * pc.nc * 16 : nullptr;
-    const __amdgpu_buffer_rsrc_t grec_rs = out_rsrc(grec, pers ? 16u * (uint32_t)pc.nc : 0u);
     if (cull && !pers) {
       cull_cells(lds_keys, nb, RLOG, RNX, RNC, KPS(W), KPS(H), tid, nt, crec);
       __syncthreads();
@@ -2945,12 +2892,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         for (int h = 0; h < UPL; ++h) {
           const int cell = min(__mul24(max(pos[h].y, 0) >> RLOG, RNX) + (max(pos[h].x, 0) >> RLOG),
                                RNC - 1);
-          // (a uniform branch: a select between the HBM and LDS pointers became flat loads)
-          if (pers)
-            rec[h] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   grec_rs, 16u * (uint32_t)cell, 0, 0));
-          else
-            rec[h] = *reinterpret_cast<const v4u32*>(crec + 16 * cell);
+          rec[h] = pers ? *reinterpret_cast<const v4u32*>(grec + 16 * cell)
+                        : *reinterpret_cast<const v4u32*>(crec + 16 * cell);
         }
 #pragma unroll
         for (int h = 0; h < UPL; ++h) {
@@ -4027,7 +3970,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   kp.u_upperf = (float)kp.upper;
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
-  kp.xcd_remap = params->xcd_remap < 0 ? 0 : 1;
+  kp.xcd_remap = params->xcd_remap < 0 ? 0 : params->xcd_remap > 1 ? 1 + (params->xcd_remap - 1) % 8 : 1;
   kp.st8 = params->compact_state;
   if (params->num_ues > 64 && params->station_culling >= 0) {  // block kernel (block_cull_params)
     const CullP cp = block_cull_params(params->num_bs, params->width, params->height,
