@@ -352,7 +352,7 @@ def test_prefetch_registers_check_on_generated_assembly():
     assert cp.violations(good) == ([], 1)
     # a 64-bit multiply-add that reads an in-flight register only as its addend's don't-care high
     # half (the result's high half dead: redefined, after an unconditional branch, before any
-    # read) is benign; with the high half read afterwards, or a conditional branch first, not
+    # read on any path) is benign; with the high half read afterwards on some path, not
     head = ("_Zk:\n\tglobal_load_dword v43, v[2:3], off ; mev-prefetch\n"
             "\tv_mad_u64_u32 v[0:1], s[8:9], s35, v7, v[42:43]\n")
     tail = "\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v43\n"
@@ -360,8 +360,11 @@ def test_prefetch_registers_check_on_generated_assembly():
     assert cp.violations(dead) == ([], 1)
     used = head + "\tv_add_u32_e32 v4, v1, v0\n" + tail
     assert cp.violations(used)[0]
-    cond = head + "\ts_cbranch_scc1 .LBB0_2\n\tds_read_u8 v1, v0\n.LBB0_2:\n" + tail
+    cond = (head + "\ts_cbranch_scc1 .LBB0_2\n\tds_read_u8 v1, v0\n.LBB0_2:\n"
+            "\tv_add_u32_e32 v4, v1, v0\n" + tail)  # (the taken branch reads the dead half)
     assert cp.violations(cond)[0]
+    both = head + "\ts_cbranch_scc1 .LBB0_2\n\tds_read_u8 v1, v0\n.LBB0_2:\n" + tail
+    assert cp.violations(both) == ([], 1)  # (no path reads it)
     text = open(cp.build_asm()).read()
     v, n = cp.violations(text)
     assert n >= 8 and v == []

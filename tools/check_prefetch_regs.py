@@ -48,12 +48,14 @@ def _split_operands(line: str):
     return parts[0], [o.strip() for o in parts[1].split(",")]
 
 
-def _dead_high_addend(op, ops, hit, lines, idx, horizon=24):
+def _dead_high_addend(op, ops, hit, lines, idx, horizon=4000):
     """A v_mad_u64_u32 / v_mad_i64_i32 whose only in-flight operand is the HIGH half of its
-    64-bit addend, with the result's high half dead (its next mention in the same basic block
-    is as the destination of an instruction that does not read it): the low 32 bits of the
-    result do not depend on the addend's high half, so the register is read for nothing (the
-    compiler's pick for a don't-care half) -- no value reaches any use."""
+    64-bit addend, with the result's high half dead on every path from it (each path redefines
+    it, as the destination of an instruction that does not read it, before any read, or ends
+    the program): the low 32 bits of the result do not depend on the addend's high half, so the
+    register is read for nothing (the compiler's pick for a don't-care half) -- no value
+    reaches any use. Conditional branches fork the walk; a label already walked is not walked
+    again (its first visit decides)."""
     if op not in ("v_mad_u64_u32", "v_mad_i64_i32") or len(ops) < 5:
         return False
     m = re.match(r"v\[(\d+):(\d+)\]$", ops[-1])
@@ -61,30 +63,45 @@ def _dead_high_addend(op, ops, hit, lines, idx, horizon=24):
     if not m or not d or hit != {int(m.group(2))}:
         return False
     hi = int(d.group(2))
-    # follow the one path from here (fall-through, unconditional branches); a conditional branch
-    # before the first mention leaves two paths: not proven
     labels = {t.split(":")[0].strip(): k for k, (_, t) in enumerate(lines)
               if re.match(r"^\.LBB\w*:", t)}
-    k, steps = idx + 1, 0
-    while k < len(lines) and steps < horizon:
-        code = lines[k][1].split(";")[0].strip()
-        k += 1
-        if not code or code.startswith(".") and not code.endswith(":") or code.endswith(":"):
-            continue
-        steps += 1
-        if code.startswith("s_cbranch"):
-            return False
-        if code.startswith("s_branch"):
-            tgt = code.split()[1]
-            if tgt not in labels:
-                return False
-            k = labels[tgt] + 1
-            continue
-        o2, ops2 = _split_operands(lines[k - 1][1])
-        if not ops2 or hi not in regs_of(",".join(ops2)):
-            continue
-        return hi in regs_of(ops2[0]) and hi not in regs_of(",".join(ops2[1:]))
-    return False
+    seen = set()
+    work = [idx + 1]
+    steps = 0
+    while work:
+        k = work.pop()
+        while k < len(lines):
+            steps += 1
+            if steps > horizon:
+                return False  # (not proven within the budget)
+            raw = lines[k][1]
+            code = raw.split(";")[0].strip()
+            k += 1
+            if code.endswith(":"):
+                if code[:-1] in seen:
+                    break
+                seen.add(code[:-1])
+                continue
+            if not code or code.startswith("."):
+                continue
+            if code.startswith("s_endpgm"):
+                break
+            if code.startswith("s_cbranch") or code.startswith("s_branch"):
+                tgt = code.split()[1]
+                if tgt not in labels:
+                    return False
+                if code.startswith("s_branch"):
+                    k = labels[tgt]
+                else:
+                    work.append(labels[tgt])
+                continue
+            o2, ops2 = _split_operands(raw)
+            if not ops2 or hi not in regs_of(",".join(ops2)):
+                continue
+            if hi in regs_of(",".join(ops2[1:])) or hi not in regs_of(ops2[0]):
+                return False  # read (or only partly written) on this path
+            break  # redefined: dead on this path
+    return True
 
 
 def check_kernel(name: str, lines):
