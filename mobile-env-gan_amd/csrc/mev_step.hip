@@ -1855,6 +1855,221 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   }
 }
 
+// ---- Software-pipelined steps (k_steps_lds2 with PIPE: one group per wavefront) ----------------
+// A step's movement (lds2_step's phases A-C) depends only on the previous step's movement, its
+// outputs (phases D-E) on nothing that comes later. With one wavefront per SIMD (a small batch:
+// 4,096 medium envs are 1,024 groups on 1,024 SIMDs) a step is one dependency chain that the SIMD
+// waits through instruction by instruction. Iteration i of the pipelined loop moves step i + 1
+// and emits step i's outputs: two independent chains in one basic block (the rare paths --
+// resets, draws past the episode table -- are uniform branches at the iteration's start, the
+// cell entry of step i is read before them), which the scheduler interleaves. Same results as
+// lds2_step bit for bit (the same operations per step, in another order across steps).
+// What a step's outputs need from its movement (the step's t, before the increment).
+struct Snap {
+  int2 pos;
+  int t;
+  bool active, valid;
+  uint64_t act_w;
+};
+
+// lds2_step's phases A-C for one group (R = 1): lazy reset, waypoint draws, movement; returns
+// the step's snapshot and advances c.t.
+template <int UC, int SCN>
+__device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, const LaneMap& m,
+                                          Ctx2& c, int e, int nok, int kval,
+                                          u128* __restrict__ lpcg, const int* __restrict__ ltab) {
+  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  const int M = KPS(tab_m);
+  const int u = m.u;
+  constexpr uint64_t kValidPat = [] {
+    uint64_t v = 0;
+    for (int q = 0; q < 64 / PC; ++q) v |= ((1ull << U) - 1ull) << (q * PC);
+    return v;
+  }();
+  int nk = nok;
+  asm volatile("" : "+s"(nk));
+  const uint64_t envok_w = nk >= G ? ~0ull : ((1ull << (uint32_t)(nk * PC)) - 1ull);
+  const uint64_t valid_w = envok_w & kValidPat;
+  const bool env_ok = m.seg < nk;
+  const int er = m.seg;
+  const bool valid = kval < nok;
+  // ---- A: lazy auto-reset (base.py:288-291) ----
+  const bool reset_env = env_ok && c.t >= KPS(t_end);
+  const bool do_reset = reset_env && valid;
+  const uint64_t rs_w = bal(c.t >= KPS(t_end)) & envok_w;
+  if (rs_w) {
+    if (reset_env) {
+      c.t = 0;
+      c.drawn = U;
+    }
+    if (do_reset) {
+      const int p = ltab[er * M + u];
+      c.pos = make_int2((int)(short)p, p >> 16);
+      c.wp = make_int2(-1, -1);
+    }
+  }
+  const int t = c.t;
+  const bool on = scn_all_active<SCN>() ||
+                  (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
+  const bool active = valid && on;
+  const uint64_t act_w = scn_all_active<SCN>() ? valid_w : bal(on) & valid_w;
+  const bool need = active && c.wp.x < 0;
+  const uint64_t mneed_w = bal(c.wp.x < 0) & act_w;
+  const uint32_t f = seg_field<PC>(mneed_w, m);
+  const int tot = __popc(f);
+  const int rank = __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)u));
+  const int k = c.drawn + rank;
+  // ---- B: waypoint draws in ue_id order (movement.py:44-47) ----
+  // every draw of the group inside the episode table: the common, branch-free path below;
+  // else (rare) every drawing lane from the stream state, as lds2_step's fallback
+  const uint64_t fb_w = bal(k >= M) & mneed_w;
+  if (fb_w) {
+    u128* const slot = lpcg + 2 * er;
+    const u128 inc = slot[1];
+    u128 s;
+    if (!(c.fl & kSok) && c.drawn > 0) {
+      s = at(const_cast<u128*>(tb.tab_st),
+             16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(min(c.drawn, M) - 1)));
+      wait_vmem();
+    } else {
+      s = slot[0];
+    }
+    if (reset_env) {
+      s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(U - 1)));
+      wait_vmem();
+    }
+    u128 s_fin = 0;
+    if ((bal(rank != 0) & mneed_w) == 0) {
+      if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
+    } else {
+      if (need) s_fin = pcg_draw_pair(s, inc, 2 * rank, tb.jump, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
+    }
+    wait_vmem();
+    const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
+    if (own_fin) slot[0] = s_fin;
+    const int fl = c.fl;
+    c.fl = tot > 0 ? (fl | kSok | kMov) : reset_env ? (fl & ~kSok) : fl;
+  } else {
+    c.fl = (tot > 0 || reset_env) ? (c.fl & ~kSok) : c.fl;
+  }
+  {  // the table's pair for every lane (clamped index), taken where a table draw is due
+    const int p = ltab[er * M + min(k, M - 1)];
+    const bool take = need && !fb_w;
+    c.wp = take ? make_int2((int)(short)p, p >> 16) : c.wp;
+  }
+  c.drawn += tot;
+  // ---- C: movement (movement.py:49-62) ----
+  constexpr bool AXF = SCN != 0;
+  constexpr bool V15 = scn_v15<SCN>();
+  const int2 pos = c.pos, wp = c.wp;
+  const int dx = wp.x - pos.x, dy = wp.y - pos.y;
+  const int ax2 = __mul24(dx, dx), ay2 = __mul24(dy, dy);
+  const int d2 = ax2 + ay2;
+  const bool arrive = d2 <= KPS(d2snap);
+  int2 npos;
+  if (V15 || KPS(axis_exact) == 2) {
+    int2 np = step_v15(pos, dx, dy, ax2, ay2);
+    asm volatile("" : "+v"(np.x), "+v"(np.y));  // (a select, not a branch on `arrive`)
+    npos = arrive ? wp : np;
+  } else {
+    const float sc = KPSF(vel_f) * __builtin_amdgcn_rsqf((float)d2);
+    const float qx = (float)dx * sc, qy = (float)dy * sc;
+    const float rx = rintf(qx), ry = rintf(qy);
+    const bool axis = dx == 0 || dy == 0;
+    bool ok = fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < KPSF(move_lim);
+    int2 np = make_int2(pos.x + (int)rx, pos.y + (int)ry);
+    if (AXF) {
+      const float vs = KPSF(vel_f);
+      const int ax = (int)rintf((float)pos.x + (dx > 0 ? vs : -vs));
+      const int ay = (int)rintf((float)pos.y + (dy > 0 ? vs : -vs));
+      if (axis) np = dy == 0 ? make_int2(ax, pos.y) : make_int2(pos.x, ay);
+      ok = ok || axis;
+    }
+    const bool xneed = active && !arrive && !ok;
+    if (bal(xneed)) {
+      if (xneed) np = move_exact(pos, dx, dy, kp.vel);
+    }
+    npos = arrive ? wp : np;
+  }
+  const bool pop = active && arrive;
+  c.pos = active ? npos : c.pos;
+  c.wp = pop ? make_int2(-1, -1) : c.wp;
+  Snap sn;
+  sn.pos = c.pos;
+  sn.t = t;
+  sn.active = active;
+  sn.valid = valid;
+  sn.act_w = act_w;
+  c.t = t + 1;
+  return sn;
+}
+
+// The cell entry of a snapshot's position (mode-3 LDS table), read ahead of the next move.
+template <int UC, int SCN>
+__device__ __forceinline__ uint32_t pipe_cell(const KParams& kp, const Snap& sn,
+                                              const char* __restrict__ lblob) {
+  const uint32_t cell = min((uint32_t)(__mul24(sn.pos.y, KPS(W)) + sn.pos.x),
+                            (uint32_t)(KPS(W) * KPS(H) - 1));
+  return *reinterpret_cast<const uint16_t*>(lblob + 2u * cell);
+}
+
+// lds2_step's phases D-E for one group from its snapshot and cell entry. The layout has no
+// cell beyond the table's ranks (0xFFFF; the host selects PIPE only when |D| <= 4,094).
+template <int UC, int SCN, bool TF>
+__device__ __forceinline__ void pipe_emit(const KParams& kp, const KOut& out, const LaneMap& m,
+                                          const Snap& sn, uint32_t ent, int e, int nok, int klead,
+                                          int row, const char* __restrict__ lblob,
+                                          int* __restrict__ hist, int* __restrict__ srow,
+                                          uint8_t* __restrict__ drow) {
+  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  const int B = KPS(B), HS = lds2_hist_stride(G, B);
+  const int u = m.u;
+  const double full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent & 4095u));
+  const int srv = sn.active && ent < 0xF000u ? (int)(ent >> 12) : -1;
+  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(UC, SCN ? scn_const(SCN).B : 0);
+  int* const h = hist + m.seg * HS;
+  int n;
+  if (PCNT) {
+    n = row_count_same(srv);
+  } else {
+    const int bin = srv >= 0 ? srv : B;
+    h[HS >= PC ? u : min(u, B)] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __hip_atomic_fetch_add(h + bin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_wave_barrier();
+    n = min(h[bin], 64);
+  }
+  const double r100 = *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n);
+  const double cc = full * r100;
+  const double rr = rint(cc);
+  const float d = (float)(cc - rr);
+  const float rf = (float)rr;
+  const bool tie = !TF && srv >= 0 && !(0.5f - fabsf(d) > __builtin_fmaf(rf, 0x1p-46f, 0x1p-25f));
+  float cf = srv >= 0 ? rf : 0.f;
+  if (!TF && bal(tie)) {
+    if (tie) cf = (float)rint((full / (double)n) * 100.0);
+  }
+  const float rate_f = cf * 0.01f;
+  const float util = sn.active ? (float)utility_f32r<SCN>(cf, rate_f, kp) : 0.f;
+  const int isum = seg_isum_rows<PC>((int)(util * 0x1p25f));
+  const int nact = __popc(seg_field<PC>(sn.act_w, m));
+  Pending up;
+  up.srv = srv;
+  up.obs = make_float4((float)sn.pos.x * KPSF(inv_w), (float)sn.pos.y * KPSF(inv_h), rate_f, util);
+  up.ui = (uint32_t)(e * U + u);
+  up.valid = sn.valid;
+  up.lead = up.done = false;
+  up.e = 0;
+  up.reward = 0.f;
+  flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
+  const bool lead = klead < nok;
+  int* const hw = h + (HS >= PC ? u : B);
+  int* sw = lead ? srow + m.seg : hw;
+  uint8_t* dw = lead ? drow + m.seg : reinterpret_cast<uint8_t*>(hw);
+  *sw = isum;
+  *dw = (uint8_t)(nact | ((sn.t + 1 >= KPS(t_end)) ? 0x80 : 0));
+}
+
 // The staged rows of k_steps_lds2: reward = (float)isum 2^-25 / nact (float32, as packed_group's
 // lean path), or the utility's lower bound without active UEs; done = bit 7.
 // Workgroup barrier for LDS data: this wave's LDS operations complete (lgkmcnt(0)), then
@@ -2102,7 +2317,10 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 // with pairs: one group per wavefront, the same step code).
 // C8: the compact UE state form (KParams::st8) as a compile-time property of the instance (the
 // prefetch registers of one form only: a runtime choice kept both sets live, and spilled them)
-template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2, bool C8 = scn_st8(SCN)>
+// PIPE: the software-pipelined step loop (pipe_move / pipe_emit; R = 1, shared layout, a layout
+// without cells beyond the mode-3 table's ranks)
+template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2, bool C8 = scn_st8(SCN),
+          bool PIPE = false>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -2199,12 +2417,34 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         } while (i < nsteps);
       };
+      if constexpr (PIPE) {
+        static_assert(R == 1 && !PE, "PIPE: one group per wavefront, a shared layout");
+        // iteration i: the cell entry of step i, the move of step i + 1, the outputs of step i
+        Snap sn = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab);
+        int i = 0, sr = 0;
+        auto emit = [&](const Snap& q, uint32_t ent) {
+          pipe_emit<UC, SCN, TF>(kp, out, m, q, ent, e[0], nok[0], klead, traj ? i : 0, lblob,
+                                 hist, sw + sr * NWG + wvu * G, dw + sr * NWG + wvu * G);
+          if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
+            flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+          ++i;
+          sr = sr + 1 == stage_rows ? 0 : sr + 1;
+        };
+        while (i + 1 < nsteps) {  // (emit advances i)
+          const uint32_t ent = pipe_cell<UC, SCN>(kp, sn, lblob);
+          const Snap nx = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab);
+          emit(sn, ent);
+          sn = nx;
+        }
+        emit(sn, pipe_cell<UC, SCN>(kp, sn, lblob));
+      } else {
 #ifdef MEV_LDS2_FULL
-      if (nok[R - 1] == G) steps(std::true_type{});
-      else steps(std::false_type{});
+        if (nok[R - 1] == G) steps(std::true_type{});
+        else steps(std::false_type{});
 #else
-      steps(std::false_type{});
+        steps(std::false_type{});
 #endif
+      }
       MEV_TS(min(3 + 3 * it, 27));
       // the state after the last step (see k_steps_packed), as unconditional buffer stores; the
       // stream state only where the slot holds it (draws past the table, mev_state.pcg): no
@@ -3386,6 +3626,8 @@ struct mev_ctx {
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
   int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
+  int dcount_h;       // mode 3: |D| of the current layout, read back by mev_update_stations
+                      // (INT_MAX: unknown); the pipelined rollout needs |D| <= 4,094
   int upl;            // k_steps_block: UEs per lane (params.ues_per_lane)
   unsigned char* crec_g;  // per-env layouts, block shape: culling records kept in HBM
   uint8_t* crec_ok;       // (mev_update_layouts; KTables::crec_g)
@@ -4033,6 +4275,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     c->tie_free = share_tie_free(tab, n, params->num_ues);
   }
   c->scn_allowed = params->scenario_constants >= 0;
+  c->dcount_h = INT_MAX;  // (mev_update_stations reads |D| back)
 
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
   c->kp.tab_m = 0;
@@ -4359,15 +4602,27 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // not its instruction count, bounds a wave that is alone on its SIMD.
     const int tg = c->p.two_groups;
     const bool full2 = pairs >= c->lds2_wgs * kLds2Waves;
-    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2))) {
-      const int R = tg == 1 ? 2 : tg == 2 ? 1 : 2;
+    // the software-pipelined one-group kernel: batches that do not fill the resident workgroups
+    // with pairs (or two_groups = 3), registered U = 15 / 30 scenarios whose layout has no cell
+    // beyond the mode-3 table's ranks. Measured on one box (200-step launches): 4,096 medium
+    // envs 116-118 vs 126 us with the one-group packed kernel; 8,192 large envs 192 vs 252 us.
+    const bool pipe = (tg == 3 || (tg == 0 && !full2)) && (kp.U == 15 || kp.U == 30) &&
+                      match_scn(c) != 0 && c->dcount_h <= 4094;
+    if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2) || pipe) &&
+        (tg != 3 || pipe)) {
+      const int R = tg == 1 ? 2 : (tg >= 2 || pipe) ? 1 : 2;
       const int units = R == 2 ? pairs : groups;  // the waves' work units
       const int nw2 = std::max(1, std::min(kLds2Waves, (units + c->lds2_wgs - 1) / c->lds2_wgs));
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
       StepsKernel k2;
       const bool c8 = kp.st8 != 0;  // (generic instances: the state form as a template flag)
-      if (R == 2)
+      if (pipe)
+        k2 = kp.U == 15 ? (tf ? k_steps_lds2<15, 1, false, true, 1, scn_st8(1), true>
+                              : k_steps_lds2<15, 1, false, false, 1, scn_st8(1), true>)
+                        : (tf ? k_steps_lds2<30, 2, false, true, 1, scn_st8(2), true>
+                              : k_steps_lds2<30, 2, false, false, 1, scn_st8(2), true>);
+      else if (R == 2)
         k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true> : k_steps_lds2<15, 1>)
                            : c8     ? k_steps_lds2<15, 0, false, false, 2, true>
                                     : k_steps_lds2<15, 0>)
@@ -4561,6 +4816,13 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        c->assoc, cells, c->dwords, c->d2max, c->rate_full,
                        reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_rate_off);
     MEV_HIP(hipGetLastError());
+    // |D| for the host's kernel choice (the pipelined rollout takes layouts without cells
+    // beyond the table's ranks): one synchronous read per layout
+    int dc = 0;
+    MEV_HIP(hipMemcpyAsync(&dc, c->dwords + c->nwords, sizeof(int), hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+    MEV_HIP(hipStreamSynchronize((hipStream_t)stream));
+    const_cast<mev_ctx*>(c)->dcount_h = dc;
   } else if (c->blob) {
     const int bytes = (cells + 1) / 2;
     hipLaunchKernelGGL(k_lds_map, dim3((bytes + 255) / 256), dim3(256), 0, (hipStream_t)stream,

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-4 GPU session 9: the pipelined kernel as the small-batch default -- full GPU tests, the
+# medium bench line (BASELINE configs[1]) and its profile.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 150 --timeout-method thread > gpurun_out/pytest_s9.log 2>&1 || { tail -30 gpurun_out/pytest_s9.log; exit 1; }
+tail -1 gpurun_out/pytest_s9.log
+timeout -k 10 300 python3 bench.py --workload mobile-medium-central-v0 --envs 4096 > gpurun_out/bench_medium.json 2> gpurun_out/bench_medium.err || { tail gpurun_out/bench_medium.err; exit 1; }
+python3 -c "import json;d=json.loads(open('gpurun_out/bench_medium.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline'].get('launch_ms'))"
+bash tools/profile.sh r04_medium --workload mobile-medium-central-v0 --envs 4096 || exit 1
