@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <type_traits>
 #include <new>
 #include <vector>
 
@@ -1872,12 +1873,38 @@ struct Snap {
   uint64_t act_w;
 };
 
-// lds2_step's phases A-C for one group (R = 1): lazy reset, waypoint draws, movement; returns
-// the step's snapshot and advances c.t.
+// The draw-table word a lane takes in its group's next step if that step neither resets nor
+// draws past the table: pair drawn + rank among the lanes without a waypoint (ue_id order),
+// read one step ahead (pipe_move issues it after its movement, so the LDS latency passes while
+// the previous step's outputs are emitted; the next pipe_move takes it from a register).
 template <int UC, int SCN>
+__device__ __forceinline__ int pipe_pre(const KParams& kp, const LaneMap& m, const Ctx2& c,
+                                        uint64_t valid_w, const int* __restrict__ ltab) {
+  constexpr int PC = pitch_of(UC);
+  const int M = KPS(tab_m);
+  const int t = c.t;
+  const bool on = scn_all_active<SCN>() ||
+                  (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
+  const uint64_t act_w = scn_all_active<SCN>() ? valid_w : bal(on) & valid_w;
+  const uint32_t f = seg_field<PC>(bal(c.wp.x < 0) & act_w, m);
+  const int k = c.drawn + __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)m.u));
+  return ltab[m.seg * M + min(k, M - 1)];
+}
+
+// lds2_step's phases A-C for one group (R = 1): lazy reset, waypoint draws, movement; returns
+// the step's snapshot and advances c.t. pre: the lane's pipe_pre word for this step, replaced
+// by the next step's.
+struct PipeNoMid {
+  __device__ void operator()() const {}
+};
+// mid(): run between the rare branches and the movement (the kernel issues the previous step's
+// output reads there, pipe_emit_front; a scheduling barrier keeps them ahead of the movement,
+// whose instructions then pass while those LDS reads are in flight).
+template <int UC, int SCN, class Mid>
 __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, const LaneMap& m,
                                           Ctx2& c, int e, int nok, int kval,
-                                          u128* __restrict__ lpcg, const int* __restrict__ ltab) {
+                                          u128* __restrict__ lpcg, const int* __restrict__ ltab,
+                                          int& pre, Mid&& mid) {
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
   const int M = KPS(tab_m);
   const int u = m.u;
@@ -1907,6 +1934,7 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
       c.pos = make_int2((int)(short)p, p >> 16);
       c.wp = make_int2(-1, -1);
     }
+    if (PC == 16) pre = pipe_pre<UC, SCN>(kp, m, c, valid_w, ltab);  // (the reset moved drawn and the waypoints)
   }
   const int t = c.t;
   const bool on = scn_all_active<SCN>() ||
@@ -1952,9 +1980,12 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
   } else {
     c.fl = (tot > 0 || reset_env) ? (c.fl & ~kSok) : c.fl;
   }
-  {  // the table's pair for every lane (clamped index), taken where a table draw is due
-    const int p = ltab[er * M + min(k, M - 1)];
+  mid();
+  if constexpr (!std::is_same_v<std::decay_t<Mid>, PipeNoMid>) __builtin_amdgcn_sched_barrier(0);
+  {  // the table's pair (16-lane segments: read a step ahead, pipe_pre), taken where a table
+     // draw is due
     const bool take = need && !fb_w;
+    const int p = PC == 16 ? pre : ltab[er * M + min(k, M - 1)];
     c.wp = take ? make_int2((int)(short)p, p >> 16) : c.wp;
   }
   c.drawn += tot;
@@ -2001,6 +2032,9 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
   sn.valid = valid;
   sn.act_w = act_w;
   c.t = t + 1;
+  // the next step's draw word, in flight from here (32-lane segments read it in the step: 212
+  // vs 207 us per 200-step launch at 8,192 large envs with it read ahead)
+  if (PC == 16) pre = pipe_pre<UC, SCN>(kp, m, c, valid_w, ltab);
   return sn;
 }
 
@@ -2015,31 +2049,53 @@ __device__ __forceinline__ uint32_t pipe_cell(const KParams& kp, const Snap& sn,
 
 // lds2_step's phases D-E for one group from its snapshot and cell entry. The layout has no
 // cell beyond the table's ranks (0xFFFF; the host selects PIPE only when |D| <= 4,094).
-template <int UC, int SCN, bool TF>
-__device__ __forceinline__ void pipe_emit(const KParams& kp, const KOut& out, const LaneMap& m,
-                                          const Snap& sn, uint32_t ent, int e, int nok, int klead,
-                                          int row, const char* __restrict__ lblob,
-                                          int* __restrict__ hist, int* __restrict__ srow,
-                                          uint8_t* __restrict__ drow) {
-  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+// Split in two around the next step's movement: the front issues the LDS reads (the full rate
+// at the cell's rank, 100 / n after the station counts), the back waits for them and finishes.
+struct EmitF {
+  double full, r100;
+  int srv, n;
+};
+template <int UC, int SCN>
+__device__ __forceinline__ EmitF pipe_emit_front(const KParams& kp, const LaneMap& m,
+                                                 const Snap& sn, uint32_t ent,
+                                                 const char* __restrict__ lblob,
+                                                 int* __restrict__ hist) {
+  constexpr int PC = pitch_of(UC), G = 64 / PC;
   const int B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
-  const double full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent & 4095u));
-  const int srv = sn.active && ent < 0xF000u ? (int)(ent >> 12) : -1;
+  EmitF f;
+  f.full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent & 4095u));
+  f.srv = sn.active && ent < 0xF000u ? (int)(ent >> 12) : -1;
   constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(UC, SCN ? scn_const(SCN).B : 0);
   int* const h = hist + m.seg * HS;
-  int n;
   if (PCNT) {
-    n = row_count_same(srv);
+    f.n = row_count_same(f.srv);
   } else {
-    const int bin = srv >= 0 ? srv : B;
+    const int bin = f.srv >= 0 ? f.srv : B;
     h[HS >= PC ? u : min(u, B)] = 0;
     __builtin_amdgcn_wave_barrier();
     __hip_atomic_fetch_add(h + bin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __builtin_amdgcn_wave_barrier();
-    n = min(h[bin], 64);
+    f.n = min(h[bin], 64);
   }
-  const double r100 = *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n);
+  f.r100 = *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)f.n);
+  return f;
+}
+
+template <int UC, int SCN, bool TF>
+__device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& out,
+                                               const LaneMap& m, const Snap& sn, const EmitF& f,
+                                               int e, int nok, int klead, int row,
+                                               int* __restrict__ hist, int* __restrict__ srow,
+                                               uint8_t* __restrict__ drow) {
+  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  const int B = KPS(B), HS = lds2_hist_stride(G, B);
+  const int u = m.u;
+  int* const h = hist + m.seg * HS;
+  const double full = f.full, r100 = f.r100;
+  const int srv = f.srv, n = f.n;
+  (void)n;
+  (void)B;
   const double cc = full * r100;
   const double rr = rint(cc);
   const float d = (float)(cc - rr);
@@ -2420,11 +2476,24 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       if constexpr (PIPE) {
         static_assert(R == 1 && !PE, "PIPE: one group per wavefront, a shared layout");
         // iteration i: the cell entry of step i, the move of step i + 1, the outputs of step i
-        Snap sn = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab);
+        constexpr uint64_t kVP = [] {
+          uint64_t v = 0;
+          for (int q = 0; q < G; ++q) v |= ((1ull << U) - 1ull) << (q * PC);
+          return v;
+        }();
+        int nk0 = nok[0];
+        asm volatile("" : "+s"(nk0));
+        int pre = PC != 16 ? 0 : pipe_pre<UC, SCN>(
+            kp, m, c[0], (nk0 >= G ? ~0ull : ((1ull << (uint32_t)(nk0 * PC)) - 1ull)) & kVP, ltab);
+        Snap sn = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab, pre, PipeNoMid{});
+        // 16-lane segments (medium: packed DPP counts) issue the outputs' LDS reads before the
+        // next movement and wait for them after it (108.5 vs 116 us per 200-step launch at 4,096
+        // medium envs); 32-lane segments (the LDS histogram's atomics) emit after the movement
+        constexpr bool SPLIT = PC == 16;
         int i = 0, sr = 0;
-        auto emit = [&](const Snap& q, uint32_t ent) {
-          pipe_emit<UC, SCN, TF>(kp, out, m, q, ent, e[0], nok[0], klead, traj ? i : 0, lblob,
-                                 hist, sw + sr * NWG + wvu * G, dw + sr * NWG + wvu * G);
+        auto emit = [&](const Snap& q, const EmitF& ef) {
+          pipe_emit_back<UC, SCN, TF>(kp, out, m, q, ef, e[0], nok[0], klead, traj ? i : 0,
+                                      hist, sw + sr * NWG + wvu * G, dw + sr * NWG + wvu * G);
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
             flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
           ++i;
@@ -2432,11 +2501,22 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         };
         while (i + 1 < nsteps) {  // (emit advances i)
           const uint32_t ent = pipe_cell<UC, SCN>(kp, sn, lblob);
-          const Snap nx = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab);
-          emit(sn, ent);
-          sn = nx;
+          if constexpr (SPLIT) {
+            EmitF ef;
+            const Snap nx = pipe_move<UC, SCN>(
+                kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab, pre,
+                [&] { ef = pipe_emit_front<UC, SCN>(kp, m, sn, ent, lblob, hist); });
+            __builtin_amdgcn_sched_barrier(0);  // (the movement ahead of the front's waits)
+            emit(sn, ef);
+            sn = nx;
+          } else {
+            const Snap nx = pipe_move<UC, SCN>(kp, tb, m, c[0], e[0], nok[0], kval, lpcg, ltab,
+                                               pre, PipeNoMid{});
+            emit(sn, pipe_emit_front<UC, SCN>(kp, m, sn, ent, lblob, hist));
+            sn = nx;
+          }
         }
-        emit(sn, pipe_cell<UC, SCN>(kp, sn, lblob));
+        emit(sn, pipe_emit_front<UC, SCN>(kp, m, sn, pipe_cell<UC, SCN>(kp, sn, lblob), lblob, hist));
       } else {
 #ifdef MEV_LDS2_FULL
         if (nok[R - 1] == G) steps(std::true_type{});
