@@ -138,9 +138,11 @@ typedef struct mev_params {
    * fastest shape the context qualifies for). Results are identical for every setting.
    *   lds_tables: rollouts of a shared layout read the association from LDS tables of mode
    *     1..3 (KTables::lds_blob in mev_step.hip), -1: from the L2 association map;
-   *   two_groups: -1: one env group per wavefront in rollout launches (else two where the
-   *     batch fills the GPU with pairs); 1 / 2: the two-group kernel with two / one groups
-   *     per wavefront at any batch size;
+   *   two_groups: -1: one env group per wavefront in rollout launches (the packed kernel);
+   *     0: two groups per wavefront where the batch fills the GPU with pairs, else the
+   *     software-pipelined one-group kernel for the registered U = 15 / 30 scenarios, else
+   *     the packed kernel; 1 / 2: the two-group kernel with two / one groups per wavefront at
+   *     any batch size; 3: the pipelined one-group kernel at any batch size (where it applies);
    *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
    *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges; 2..8: the
    *     ranges rotated by xcd_remap - 1 XCDs, a placement experiment);
@@ -288,7 +290,9 @@ int mev_restore_stream_state(const mev_ctx* ctx, const mev_state* st, const uint
 
 /* Shared station layout (bs_per_env = 0): (re)derive the association keys the step kernel
  * uses from bs_xy (device int32 [B][2]). Called by mev_reset; call it after changing the
- * shared layout between resets. No-op for per-env layouts. Stream-ordered. */
+ * shared layout between resets. No-op for per-env layouts. Stream-ordered; with the compact
+ * LDS tables (mode 3) it then waits for the stream once: the host reads back how many distinct
+ * serving distances the layout has (the rollout kernels' choice and LDS sizes depend on it). */
 int mev_update_stations(const mev_ctx* ctx, const int32_t* bs_xy, void* stream);
 
 /* Per-env station layouts (bs_per_env = 1): rebuild what the step kernels keep per env from

@@ -58,7 +58,8 @@ class EngineParams:
     qoe_low: float = 0.0   # low-QoE threshold of the per-episode QoE statistics
     # launch-shape overrides (mev_params; 0 = automatic, results identical for every setting):
     lds_tables: int = 0          # -1 L2 association map, 1..3 that LDS table mode
-    two_groups: int = 0          # -1 one env group per wavefront in rollouts
+    two_groups: int = 0          # -1 packed one-group rollouts; 1 / 2 two-group kernel (2 / 1 groups
+                                 # per wave); 3 pipelined one-group kernel (mev.h)
     stage_rows: int = 0          # > 0: at most that many staged per-env rows per window
     xcd_remap: int = 0           # -1 blocks in dispatch order
     scenario_constants: int = 0  # -1 generic kernel instances only
