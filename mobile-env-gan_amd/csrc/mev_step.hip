@@ -4720,9 +4720,22 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                                     : k_steps_lds2<30, 0, false, false, 1>);
       const int blocks = std::min((units + nw2 - 1) / nw2, c->lds2_wgs);
       const int G = kp.envs_per_wave;
-      const int srows = std::min(c->stage_rows2, nsteps);
-      const size_t sh = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R) +
-                        (((size_t)srows * nw2 * G * R * 5 + 3) & ~(size_t)3);
+      // staged rows: c->stage_rows2 (the count that fits beside 16 waves of two groups), or for
+      // one group of 16-lane segments per wave as many as fit beside this launch's waves: 4,096
+      // medium envs, 4 waves per workgroup, then flush once per 200-step launch instead of every
+      // 17 rows (104.5 vs 108.5 us per launch). Not for 32-lane segments: larger windows made
+      // those launches slower (8,192 large envs, pipelined: 270 vs 206 us; 65,536 with two
+      // groups per wave and 126 rows: 1.72 vs 1.45 ms), all interleaved on one box.
+      const size_t wave_b = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R);
+      const size_t row_b = (size_t)nw2 * G * R * 5;
+      int fit = c->stage_rows2;
+      if (R == 1 && kp.U == 15) {
+        fit = wave_b + row_b + 4 <= (size_t)kLds2BytesPerWG
+                  ? (int)(((size_t)kLds2BytesPerWG - wave_b - 4) / row_b) : 1;
+        if (c->stage_cap > 0) fit = std::min(fit, c->stage_cap);
+      }
+      const int srows = std::max(1, std::min(fit, nsteps));
+      const size_t sh = wave_b + (((size_t)srows * row_b + 3) & ~(size_t)3);
       launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
