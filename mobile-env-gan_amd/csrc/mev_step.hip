@@ -486,6 +486,7 @@ constexpr int kLdsWaves = MEV_LDS_WAVES;
 #endif
 constexpr int kLds2Waves = MEV_LDS2_WAVES;
 constexpr int kLds2BytesPerWG = 160 * 1024;
+constexpr int kLds2Window = 3;  // staged rows per window of the two-group rollout (see its launch)
 __host__ __device__ constexpr int lds_waves(int ldsm) {
   return ldsm >= 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
 }
@@ -4728,7 +4729,14 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       // groups per wave and 126 rows: 1.72 vs 1.45 ms), all interleaved on one box.
       const size_t wave_b = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R);
       const size_t row_b = (size_t)nw2 * G * R * 5;
-      int fit = c->stage_rows2;
+      // Two groups per wave: a window of 3 rows. Each flush is a workgroup barrier, and one
+      // every 3 steps keeps the workgroup's 16 waves -- adjacent envs -- in step, so their
+      // trajectory stores reach the memory together: 168.8 vs 175 us per 20-step and 1.49 vs
+      // 1.64 ms per 200-step launch at 65,536 large envs against the 47 rows that fit
+      // (windows of 1 / 2 / 4 / 8 / 16 rows: 183 / 170.6 / 168.6 / 168 / 172.7 us and
+      // 1.58 / 1.47 / 1.50 / 1.55 / 1.59 ms; interleaved on one box)
+      // (mev_params.stage_rows > 0 overrides: A/B of window lengths)
+      int fit = R == 2 && c->stage_cap <= 0 ? std::min(c->stage_rows2, kLds2Window) : c->stage_rows2;
       if (R == 1 && kp.U == 15) {
         fit = wave_b + row_b + 4 <= (size_t)kLds2BytesPerWG
                   ? (int)(((size_t)kLds2BytesPerWG - wave_b - 4) / row_b) : 1;
