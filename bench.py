@@ -546,7 +546,8 @@ def main():
                           "basis": "SURVEY.md 8d canonical bytes per env-step x E, one-step "
                                    "launch (make().step(), mev_step(1))",
                           "frac_basis": "canonical: frac counts SURVEY 8d's bytes, which the "
-                                        "launch does not all move (int16 state); "
+                                        "launch does not all move (compact uint8 / int16 "
+                                        "UE state); "
                                         "traffic_frac = the PMC bytes it moves / peak"})
 
     if rank == 0:
