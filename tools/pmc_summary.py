@@ -66,18 +66,29 @@ def main():
     summary = {"tag": tag, "workload": workload, "envs": envs, "launch": launch,
                "bench_args": extra}
     stats = glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    full = None  # the launch's kernel: of the matching instances, the one with the most time
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-        for row in rows_of(stats[0], "Name"):
-            if kre.search(row["Name"]):
-                summary["kernel"] = re.sub(r"\(\w+::KParams.*", "", row["Name"])
-                summary["stats_avg_ns"] = float(row["AverageNs"])
-                summary["stats_calls"] = int(row["Calls"])
+        rows = [r for r in rows_of(stats[0], "Name") if kre.search(r["Name"])]
+        if rows:
+            row = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+            full = row["Name"]
+            summary["kernel"] = re.sub(r"\(\w+::KParams.*", "", row["Name"])
+            summary["stats_avg_ns"] = float(row["AverageNs"])
+            summary["stats_calls"] = int(row["Calls"])
+
+    def mine(name):  # (another instance -- e.g. the warmup's one-step launch -- is not counted)
+        return kre.search(name) and (full is None or name.strip() == full.strip())
+
+    # (a trace whose names do not match the summary's exactly: every matching instance, as before)
+    if full is not None and not any(mine(r.get("Kernel_Name", "")) for r in
+                                    rows_of(os.path.join(out, "kt", "**", "*kernel_trace.csv"), "")):
+        full = None
 
     # timed region from the trace: the last launches of the kernel
     trace = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
                    for r in rows_of(os.path.join(out, "kt", "**", "*kernel_trace.csv"), "")
-                   if kre.search(r.get("Kernel_Name", "")))
+                   if mine(r.get("Kernel_Name", "")))
     steps_per_launch = chunk if launch == "fused" else 1
     parts = 2 if launch == "split" else 1
     n_timed = -(-steps // steps_per_launch) * parts  # whole chunks + the remainder launch
@@ -95,7 +106,7 @@ def main():
     for name in ("fetch", "write", "sq", "sq2", "sq3"):
         vals = {}
         for r in rows_of(os.path.join(out, name, "**", "*counter_collection.csv"), ""):
-            if kre.search(r.get("Kernel_Name", "")):
+            if mine(r.get("Kernel_Name", "")):
                 vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         for k, v in vals.items():
             pmc[k] = sum(v) / len(v)
