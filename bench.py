@@ -67,8 +67,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (whole node), mobile-large-central-v0 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-DTYPE = ("mixed: int16/int32 positions and association, f64 rate and cents, "
-         "f32 obs/utility, int32 fixed-point reward sum")
+
+
+def dtype_string(state_bytes_per_ue: int) -> str:
+    """The arithmetic types the timed path computes in: the UE state rows in their kernel form
+    (mev_state_bytes_per_ue: 4 = the compact uint8 x4 rows of maps <= 255 per side, every
+    registered scenario; 8 = int16 x4), int32 squared distances and association keys, float64
+    rates and ResourceFair cents, float32 obs and utility, and the reward as an int32 2^-25
+    fixed-point sum over the env's UEs (float32 at the end)."""
+    state = ("uint8x4 compact UE state (x, y, waypoint; 255 = none)" if state_bytes_per_ue == 4
+             else "int16x4 UE state (x, y, waypoint)")
+    return (f"mixed: {state}, int32 d2 / association keys, f64 rate and cents, f32 obs / "
+            "utility, int32 2^-25 fixed-point reward sum -> f32")
 
 
 def algorithmic_bytes_per_env_step(num_ues: int, per_env_bs: bool, num_bs: int) -> int:
@@ -586,7 +596,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": DTYPE,
+            "dtype": dtype_string(getattr(eng, "state_bytes_per_ue", 4)),
             "host_wait": args.host_wait,
             "data": "synthetic (seeded PCG64 streams, build-defined BS layout)",
             "config": {"workload": args.workload, "envs_per_gpu": E, "global_envs": world * E,

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 20
+#define MEV_ABI_VERSION 21
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -244,6 +244,18 @@ int mev_share_cents(const mev_ctx* ctx, int32_t nmax, int32_t path, double* dst,
  * registered scenario s compiled with its parameters as constants (chosen when every value
  * matches; mev_params.scenario_constants = -1 forces the generic instance). */
 int mev_rollout_instance(const mev_ctx* ctx);
+
+/* Diagnostic (tests, A/B tools): the step kernel the context's last mev_step / mev_rollout call
+ * launched (0 before any). Every kind computes the same results; the choice depends on the
+ * batch, the launch length, the output set and the layout. */
+#define MEV_KIND_PACKED_STEP 1   /* one launch per step, one lane per UE (k_step_packed) */
+#define MEV_KIND_PACKED_FUSED 2  /* fused steps, one env group per wavefront (k_steps_packed) */
+#define MEV_KIND_LDS2_TWO 3      /* fused, two env groups per wavefront (k_steps_lds2, R = 2) */
+#define MEV_KIND_LDS2_ONE 4      /* fused, one group per wavefront (k_steps_lds2, R = 1) */
+#define MEV_KIND_LDS2_PIPE 5     /* fused, software-pipelined one-group loop (k_steps_lds2 PIPE) */
+#define MEV_KIND_LDS2_PERENV 6   /* fused, per-env layouts, two groups per wavefront */
+#define MEV_KIND_BLOCK 7         /* one workgroup per env (k_steps_block) */
+int mev_last_launch_kind(const mev_ctx* ctx);
 
 /* 1 when the context's rate table needs no tie test in the ResourceFair share of the kernels
  * that form it from a 100/n table: for every entry and every share count n <= num_ues,

@@ -1283,13 +1283,18 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
 // MI355X_MICROARCH.md "Workgroup dispatch"); with the remap the blocks that share an XCD
 // (equal blockIdx % 8) cover one contiguous range, so the per-env rows that several blocks
 // write partially (t, reward, done, pcg) are merged in one L2 instead of eight. Bijective
-// for any grid size. Speed only: any block order is correct.
+// for any grid size. Speed only: any block order is correct. remap > 1 (dev): the slots are
+// shifted cyclically by the start of range remap - 1, so XCD x covers the range XCD
+// x + remap - 1 would (whole ranges when 8 divides the grid) -- still a bijection.
 __device__ __forceinline__ int block_slot(int remap) {
   const int orig = blockIdx.x;
   if (!remap) return orig;
-  const int nwg = gridDim.x;
-  const int xcd = (orig + remap - 1) & 7, q = nwg >> 3, r = nwg & 7;  // (remap > 1: rotated, dev)
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+  auto base = [&](int x) { return x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q; };
+  const int s = base(orig & 7) + (orig >> 3);
+  if (remap == 1) return s;
+  const int t = s + base(remap - 1);
+  return t >= nwg ? t - nwg : t;
 }
 
 // 16-byte pieces of the LDS blob a rollout copies: all of it, or (mode 3) up to the rates over D
@@ -3707,8 +3712,12 @@ struct mev_ctx {
   hipEvent_t ev_fork, ev_join;
   int scn_allowed;    // MEV_SCN at mev_create (0: the generic rollout instance only)
   int tie_free;       // share_tie_free: the rounded share needs no tie test for this table
-  int dcount_h;       // mode 3: |D| of the current layout, read back by mev_update_stations
-                      // (INT_MAX: unknown); the pipelined rollout needs |D| <= 4,094
+  mutable int dcount_h;  // mode 3: |D| of the current layout (INT_MAX: unknown); the
+                         // pipelined rollout needs |D| <= 4,094
+  int* dcount_pin;       // pinned host word mev_update_stations copies |D| into, stream-ordered
+  hipEvent_t ev_dcount;  // recorded after that copy; the first launch that needs |D| waits on it
+  mutable int dcount_pending;
+  mutable int last_kind;  // mev_last_launch_kind: the kernel the last step / rollout call ran
   int upl;            // k_steps_block: UEs per lane (params.ues_per_lane)
   unsigned char* crec_g;  // per-env layouts, block shape: culling records kept in HBM
   uint8_t* crec_ok;       // (mev_update_layouts; KTables::crec_g)
@@ -4158,7 +4167,11 @@ static int build_het(mev_ctx* c) {
       int64_t n;
       const size_t off = all.size();
       if (p->rate_table) {
-        const int64_t a = p->rate_table_offsets[pi], b = p->rate_table_offsets[pi + 1];
+        // one class pair (per-UE velocities only): validate() requires no offsets, the whole
+        // table is that pair's
+        const bool whole = !p->rate_table_offsets && NB * NU == 1;
+        const int64_t a = whole ? 0 : p->rate_table_offsets[pi];
+        const int64_t b = whole ? p->rate_table_len : p->rate_table_offsets[pi + 1];
         n = b - a;
         all.insert(all.end(), p->rate_table + a, p->rate_table + b);
       } else {
@@ -4357,6 +4370,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   }
   c->scn_allowed = params->scenario_constants >= 0;
   c->dcount_h = INT_MAX;  // (mev_update_stations reads |D| back)
+  c->dcount_pending = 0;
 
   // ---- episode draw table (packed shape, movement re-seeded every episode) ----
   c->kp.tab_m = 0;
@@ -4420,6 +4434,10 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     if (rc) {
       return rc;
     }
+  }
+  if (c->blob && c->kp.lds_mode == 3) {  // |D| of each layout, read back without a stream sync
+    MEV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->dcount_pin), sizeof(int), hipHostMallocDefault));
+    MEV_HIP(hipEventCreateWithFlags(&c->ev_dcount, hipEventDisableTiming));
   }
 
   // ---- utility table over rounded rates ----
@@ -4500,6 +4518,8 @@ void mev_destroy(mev_ctx* c) {
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_dcount) (void)hipEventDestroy(c->ev_dcount);
+  if (c->dcount_pin) (void)hipHostFree(c->dcount_pin);
   delete c;
 }
 
@@ -4518,6 +4538,8 @@ int mev_state_bytes_per_ue(const mev_ctx* c) { return c ? (c->kp.st8 ? 4 : 8) : 
 const double* mev_rate_table(const mev_ctx* c) { return c ? c->rate_full : nullptr; }
 
 int mev_share_tie_free(const mev_ctx* c) { return c ? c->tie_free : MEV_EINVAL; }
+
+int mev_last_launch_kind(const mev_ctx* c) { return c ? c->last_kind : MEV_EINVAL; }
 
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
@@ -4626,6 +4648,17 @@ static int launch_packed_split(const mev_ctx* c, const KState& ks, const KOut& k
                                const KTables& tb, int nsteps, bool traj, hipStream_t stream,
                                StepKernel k, size_t shmem, int groups);
 
+// |D| of the current shared layout (mode 3), INT_MAX when unknown: waits for the pinned copy
+// mev_update_stations issued (normally long complete when the first rollout asks)
+static int layout_dcount(const mev_ctx* c) {
+  if (c->dcount_pending) {
+    if (hipEventSynchronize(c->ev_dcount) != hipSuccess) return INT_MAX;
+    c->dcount_h = *c->dcount_pin;
+    c->dcount_pending = 0;
+  }
+  return c->dcount_h;
+}
+
 // Packed step kernels of `nsteps` steps. Two-half shape: the first half of the groups runs on
 // the caller's stream, the second on c->aux (forked from and joined back into the caller's
 // stream); the halves are independent envs, so the two streams overlap freely.
@@ -4672,6 +4705,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       launch_k(k2, dim3(blocks), dim3(64 * kLds2Waves), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
+      c->last_kind = MEV_KIND_LDS2_PERENV;
       return MEV_OK;
     }
     // two groups per wavefront once the pairs fill every resident workgroup, else the
@@ -4688,7 +4722,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // beyond the mode-3 table's ranks. Measured on one box (200-step launches): 4,096 medium
     // envs 116-118 vs 126 us with the one-group packed kernel; 8,192 large envs 192 vs 252 us.
     const bool pipe = (tg == 3 || (tg == 0 && !full2)) && (kp.U == 15 || kp.U == 30) &&
-                      match_scn(c) != 0 && c->dcount_h <= 4094;
+                      match_scn(c) != 0 && layout_dcount(c) <= 4094;
     if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2) || pipe) &&
         (tg != 3 || pipe)) {
       const int R = tg == 1 ? 2 : (tg >= 2 || pipe) ? 1 : 2;
@@ -4747,6 +4781,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
+      c->last_kind = pipe ? MEV_KIND_LDS2_PIPE : R == 2 ? MEV_KIND_LDS2_TWO : MEV_KIND_LDS2_ONE;
       return MEV_OK;
     }
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);
@@ -4771,11 +4806,13 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     launch_k(kf, dim3(blocks), dim3(64 * nw), shmem_f + (stg ? stage_lds_bytes(kp, srows, nw) : 0),
              stream, ev, kp, ks, ko, tb, groups, nsteps, traj ? 1 : 0, srows);
     MEV_HIP(hipGetLastError());
+    c->last_kind = MEV_KIND_PACKED_FUSED;
     return MEV_OK;
   }
   // (several kernels: the timing events around them)
   if (ev.start) MEV_HIP(hipEventRecord(ev.start, stream));
   const int rc = launch_packed_split(c, ks, ko, tb, nsteps, traj, stream, k, shmem, groups);
+  c->last_kind = MEV_KIND_PACKED_STEP;
   if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, stream));
   return rc;
 }
@@ -4851,6 +4888,7 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
     if (ev.stop) MEV_HIP(hipEventRecord(ev.stop, stream));
   }
   MEV_HIP(hipGetLastError());
+  c->last_kind = MEV_KIND_BLOCK;
   return MEV_OK;
 }
 
@@ -4918,12 +4956,12 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        reinterpret_cast<uint8_t*>(c->blob), c->kp.lds_rate_off);
     MEV_HIP(hipGetLastError());
     // |D| for the host's kernel choice (the pipelined rollout takes layouts without cells
-    // beyond the table's ranks): one synchronous read per layout
-    int dc = 0;
-    MEV_HIP(hipMemcpyAsync(&dc, c->dwords + c->nwords, sizeof(int), hipMemcpyDeviceToHost,
-                           (hipStream_t)stream));
-    MEV_HIP(hipStreamSynchronize((hipStream_t)stream));
-    const_cast<mev_ctx*>(c)->dcount_h = dc;
+    // beyond the table's ranks): copied to pinned memory in stream order; the first launch
+    // whose choice depends on it waits for that copy's event (layout_dcount), nothing else does
+    MEV_HIP(hipMemcpyAsync(c->dcount_pin, c->dwords + c->nwords, sizeof(int),
+                           hipMemcpyDeviceToHost, (hipStream_t)stream));
+    MEV_HIP(hipEventRecord(c->ev_dcount, (hipStream_t)stream));
+    c->dcount_pending = 1;
   } else if (c->blob) {
     const int bytes = (cells + 1) / 2;
     hipLaunchKernelGGL(k_lds_map, dim3((bytes + 255) / 256), dim3(256), 0, (hipStream_t)stream,

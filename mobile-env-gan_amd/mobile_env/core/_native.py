@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -25,7 +25,7 @@ MEV_ECHANNEL = -1001
 EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes", "mev_state_bytes_per_ue",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations", "mev_update_layouts", "mev_build_rate_table", "mev_share_cents",
-           "mev_rollout_instance", "mev_share_tie_free",
+           "mev_rollout_instance", "mev_share_tie_free", "mev_last_launch_kind",
            "mev_reset", "mev_prepare_draws", "mev_sync_stream_state", "mev_restore_stream_state", "mev_step", "mev_rollout", "mev_rollout_timed", "mev_strerror", "mev_last_hip_error")
 
 
@@ -147,6 +147,8 @@ def lib():
         L.mev_rollout_instance.restype = C.c_int
         L.mev_share_tie_free.argtypes = [C.c_void_p]
         L.mev_share_tie_free.restype = C.c_int
+        L.mev_last_launch_kind.argtypes = [C.c_void_p]
+        L.mev_last_launch_kind.restype = C.c_int
         L.mev_strerror.argtypes = [C.c_int]
         L.mev_strerror.restype = C.c_char_p
         L.mev_last_hip_error.restype = C.c_char_p

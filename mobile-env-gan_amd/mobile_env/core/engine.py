@@ -297,12 +297,21 @@ class StepEngine:
     @property
     def ue_state(self):
         """UE state rows [E,U,4] int16 {x, y, wx, wy} (wx < 0: no waypoint): the kernels' rows
-        (mev_state.ue_state) in their int16 form -- a decoded copy where the context keeps the
-        compact uint8 form (255 = -1; maps <= 255 per side). Write rows with restore_state."""
+        (mev_state.ue_state) in their int16 form -- a decoded COPY where the context keeps the
+        compact uint8 form (255 = -1; maps <= 255 per side, the default there), so writes to it
+        are not seen by the kernels. Write rows with restore_state (or through state_rows)."""
         if not self._u8:
             return self._ue_raw
         v = self._ue_raw.to(torch.int16)
         return torch.where(v == 255, torch.full_like(v, -1), v)
+
+    @property
+    def state_rows(self):
+        """The kernels' own UE state buffer (mev_state.ue_state) in its own form -- uint8 [E,U,4]
+        with 255 for -1 (compact_state) or int16 [E,U,4] -- a writable view: writes reach the
+        next launch. After writing mid-episode rows, declare the stream states with
+        restore_state if the envs' pcg rows changed too."""
+        return self._ue_raw
 
     @property
     def state_bytes_per_ue(self) -> int:
@@ -311,7 +320,8 @@ class StepEngine:
 
     @property
     def ue_xy(self):
-        """UE positions [E,U,2] (int16; a view of the rows in the int16 form)."""
+        """UE positions [E,U,2] int16: a view of the rows in the int16 form, a decoded copy in
+        the compact form (see ue_state)."""
         return self._ue_raw[..., :2] if not self._u8 else self._ue_raw[..., :2].to(torch.int16)
 
     @property
@@ -348,6 +358,16 @@ class StepEngine:
     def rollout_instance(self) -> int:
         """Rollout kernel instance: 0 generic, s > 0 registered scenario s with constants."""
         return int(self._lib.mev_rollout_instance(self._ctx))
+
+    #: mev_last_launch_kind codes (include/mev.h MEV_KIND_*)
+    LAUNCH_KINDS = {0: None, 1: "packed_step", 2: "packed_fused", 3: "lds2_two_groups",
+                    4: "lds2_one_group", 5: "lds2_pipelined", 6: "lds2_per_env", 7: "block"}
+
+    @property
+    def last_launch_kind(self) -> "str | None":
+        """The step kernel the last step() / rollout() launched (mev_last_launch_kind): every
+        kind computes the same results; tests use it to pin which kernel they checked."""
+        return self.LAUNCH_KINDS[int(self._lib.mev_last_launch_kind(self._ctx))]
 
     @property
     def share_tie_free(self) -> bool:

@@ -1,0 +1,120 @@
+"""GPU regression tests for defects found in review.
+
+* per-UE velocities with a single channel class (mev_params.ue_velocity set, no class arrays,
+  one rate table without offsets): mev_create used to dereference the absent rate-table
+  offsets; built through EngineParams and through the facade's lowering (UserEquipment objects
+  that differ only in velocity, entities.py:33-45), checked against the oracle;
+* xcd_remap rotations 2..8 on grids that are not a multiple of 8 workgroups: every env range
+  must be covered exactly once (block_slot is a bijection), so every setting gives the
+  outputs of the default order, for the one-step kernel and the fused rollouts;
+* mev_update_stations no longer blocks the host: a layout change followed by a rollout still
+  selects the kernel that depends on the layout's distance set (|D|, read back without a
+  stream sync) and gives the oracle's results.
+Reference: movement.py:42-62 (per-UE velocity), base.py:230-296.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_rollout_vs_oracle, assert_step_vs_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _velocity_users(U):
+    return [1.0 + 0.75 * (u % 7) for u in range(U)]
+
+
+@pytest.mark.parametrize("via", ["params", "lowering"])
+def test_per_ue_velocity_single_class_vs_oracle(via):
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS["large"]
+    U, B, E = L["num_ues"], len(L["bs"]), 300
+    vel = _velocity_users(U)
+    if via == "params":
+        p = EngineParams(num_envs=E, num_ues=U, num_bs=B, ue_velocity=vel)
+    else:
+        from mobile_env.core import lowering
+        from mobile_env.core.base import MComCore
+        from mobile_env.core.entities import BaseStation, UserEquipment
+        base = MComCore.default_config()
+        stations = [BaseStation(i, (int(x), int(y)), **base["bs"])
+                    for i, (x, y) in enumerate(L["bs"])]
+        users = [UserEquipment(i, **dict(base["ue"], velocity=vel[i])) for i in range(U)]
+        core = MComCore(stations, users, config={})
+        p = lowering.lower(num_envs=E, stations=stations, users=users,
+                           arrival=core.arrivalModel, channel=core.channelModel,
+                           scheduler=core.schedulerModel, movement=core.movementModel,
+                           utility=core.utilityModel, ep_max_time=core.EP_MAX_TIME,
+                           first_step_active=True)
+        assert p.ue_velocity is not None and not p.heterogeneous
+    seeds = 4242 + np.arange(E)
+    eng = StepEngine(p, L["bs"], seeds, device="cuda")
+    ob = OracleBatch(OracleParams(ue_velocity=vel), L["bs"], U, seeds)
+    for s in range(23):  # one-step launches across the episode reset
+        eng.step()
+        o = ob.step()
+        assert_step_vs_oracle(o, eng.obs.cpu().numpy(), eng.serving.cpu().numpy(),
+                              eng.reward.cpu().numpy(), eng.done.cpu().numpy(), where=f"step {s}")
+    tr = eng.rollout(25)  # and a fused rollout from there
+    assert_rollout_vs_oracle(tr, ob, 25)
+    eng.close()
+
+
+@pytest.mark.parametrize("size,E,nsteps", [("large", 8 * 13 + 3, 1), ("large", 3001, 45),
+                                           ("medium", 4096 + 40, 45), ("large", 70001, 20)])
+def test_xcd_remap_rotations_identical(size, E, nsteps):
+    """xcd_remap -1 (dispatch order), 1 (default), 2..8 (rotated ranges) on grids that 8 does
+    not divide: every step's outputs and the final state bit-identical."""
+    import torch
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    L = LAYOUTS[size]
+    first = None
+    kinds = set()
+    for remap in (-1, 1, 2, 3, 4, 5, 6, 7, 8):
+        p = EngineParams(num_envs=E, num_ues=L["num_ues"], num_bs=len(L["bs"]), xcd_remap=remap)
+        eng = StepEngine(p, L["bs"], 17 + np.arange(E), device="cuda")
+        if nsteps == 1:
+            rows = []
+            for _ in range(22):
+                eng.step()
+                rows += [eng.obs.clone(), eng.serving.clone(), eng.reward.clone(), eng.done.clone()]
+        else:
+            tr = eng.rollout(nsteps)
+            rows = [tr.obs, tr.serving, tr.reward, tr.done]
+        kinds.add(eng.last_launch_kind)
+        torch.cuda.synchronize()
+        run = [x.cpu() for x in rows] + [x.cpu().clone() for x in (eng.ue_state, eng.t)]
+        eng.close()
+        if first is None:
+            first = run
+        else:
+            for a, b in zip(first, run):
+                assert torch.equal(a, b), f"xcd_remap={remap}"
+    assert len(kinds) == 1
+
+
+def test_layout_change_then_pipelined_rollout_vs_oracle():
+    """A shared layout changed between rollouts (mev_update_stations, no host sync): the
+    pipelined kernel's choice reads the new layout's |D| and the outputs follow the new
+    layout (oracle on the new layout, from the engine's state at the change)."""
+    import torch
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS["medium"]
+    U, B, E = L["num_ues"], len(L["bs"]), 512
+    seeds = 9 + np.arange(E)
+    eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B), L["bs"], seeds,
+                     device="cuda")
+    eng.rollout(20)  # one whole episode on the registered layout
+    assert eng.last_launch_kind == "lds2_pipelined"
+    new_bs = (np.asarray(L["bs"]) + 7) % 200
+    eng.set_bs_layout(torch.as_tensor(new_bs, dtype=torch.int32))
+    tr = eng.rollout(45)  # the next episodes: lazy reset, then the new layout throughout
+    assert eng.last_launch_kind in ("lds2_pipelined", "packed_fused")
+    ob = OracleBatch(OracleParams(), new_bs.tolist(), U, seeds)
+    assert_rollout_vs_oracle(tr, ob, 45)
+    eng.close()

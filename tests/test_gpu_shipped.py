@@ -1,0 +1,99 @@
+"""GPU parity of the kernels the BASELINE.json configs actually ship, against the oracle directly.
+
+The launch the engine picks depends on the batch size, the launch length and the scenario's
+parameters (scenario-constant instances, tie-free share, compact state, pipelined loop), so a
+kernel instance can be selected by a registered scenario at its own batch size and nowhere else.
+These tests run ``make(<registered id>, num_envs=<BASELINE size>)`` with its automatic choice,
+assert which kernel ran (``StepEngine.last_launch_kind``, mev_last_launch_kind), and compare
+every step's outputs with the oracle (oracle/vec.py, pinned to the reference's fixtures):
+
+* BASELINE configs[1]: mobile-medium-central-v0 at 4,096 envs -> the software-pipelined
+  one-group rollout, U = 15 / velocity 1.5 scenario constants, tie-free share -- every env,
+  45 steps (two episode resets); and the same batch forced onto the one-group packed kernel;
+* BASELINE configs[2] (the bench): mobile-large-central-v0 at 65,536 envs -> the two-group
+  scenario kernel; every 16th env (4,096 of them) against the oracle run on those envs' seeds
+  -- envs are independent, so the subset comparison is exact;
+* the Gym step() launch of both (mev_step(1), one launch per step).
+
+Bars (north_star): positions, serving, done bit-exact; float32 rate / utility / reward within
+1e-5 relative (rewards of magnitude >= 1e-3 with atol 0, helpers.assert_step_vs_oracle).
+Reference: base.py:230-296 (step), movement.py:42-62 (RandomWaypoint), channels.py:133-146.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_rollout_vs_oracle, assert_step_vs_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(size, seeds, vel=1.5):
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS[size]
+    return OracleBatch(OracleParams(velocity=vel), L["bs"], L["num_ues"], np.asarray(seeds))
+
+
+@pytest.mark.parametrize("two_groups,kind", [(0, "lds2_pipelined"), (-1, "packed_fused")])
+def test_medium_4096_shipped_rollout_vs_oracle(two_groups, kind):
+    """BASELINE configs[1] with the kernel make() picks for it (and the packed fallback): one
+    45-step rollout of every one of the 4,096 envs against the oracle, step by step."""
+    import mobile_env
+    E, n = 4096, 45
+    env = mobile_env.make("mobile-medium-central-v0", num_envs=E, device="cuda:0", seed=5,
+                          two_groups=two_groups)
+    env.reset()
+    eng = env.engine
+    assert eng.rollout_instance == 1 and eng.share_tie_free and eng.state_bytes_per_ue == 4
+    tr = eng.rollout(n)
+    assert eng.last_launch_kind == kind
+    o = assert_rollout_vs_oracle(tr, _oracle("medium", env.seeds.numpy()), n)
+    np.testing.assert_array_equal(eng.ue_xy.cpu().numpy(), o["xy"])
+    env.close()
+
+
+def test_large_65536_bench_rollout_strided_vs_oracle():
+    """The bench's own launch (BASELINE configs[2]: 65,536 mobile-large envs, the two-group
+    scenario-constant kernel): one 45-step rollout, every 16th env against the oracle."""
+    import mobile_env
+    import torch
+    E, n, stride = 65536, 45, 16
+    env = mobile_env.make("mobile-large-central-v0", num_envs=E, device="cuda:0", seed=1000)
+    env.reset()
+    eng = env.engine
+    assert eng.rollout_instance == 2 and eng.share_tie_free
+    tr = eng.rollout(n)
+    assert eng.last_launch_kind == "lds2_two_groups"
+    idx = np.arange(0, E, stride)
+    ob = _oracle("large", env.seeds.numpy()[idx])
+    o = assert_rollout_vs_oracle(tr, ob, n, env_idx=idx)
+    ti = torch.as_tensor(idx, device=eng.device)
+    np.testing.assert_array_equal(eng.ue_xy.index_select(0, ti).cpu().numpy(), o["xy"])
+    del tr
+    env.close()
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("env_id,size,E,stride", [("mobile-medium-central-v0", "medium", 4096, 1),
+                                                  ("mobile-large-central-v0", "large", 65536, 16)])
+def test_gym_step_shipped_vs_oracle(env_id, size, E, stride):
+    """The Gym surface (VectorMobileEnv.step -> mev_step(1)) at the BASELINE batch sizes: 23
+    one-step launches (crossing the episode reset), checked against the oracle every step."""
+    import mobile_env
+    import torch
+    env = mobile_env.make(env_id, num_envs=E, device="cuda:0", seed=77)
+    env.reset()
+    idx = np.arange(0, E, stride)
+    ti = torch.as_tensor(idx, device=env.device)
+    ob = _oracle(size, env.seeds.numpy()[idx])
+    U = env.num_ues
+    for s in range(23):
+        obs, reward, term, trunc, info = env.step()
+        assert env.engine.last_launch_kind == "packed_step"
+        o = ob.step()
+        obs = obs.view(E, U, 4).index_select(0, ti).cpu().numpy()
+        assert_step_vs_oracle(o, obs, info["serving"].index_select(0, ti).cpu().numpy(),
+                              reward.index_select(0, ti).cpu().numpy(),
+                              trunc.index_select(0, ti).cpu().numpy(), where=f"step {s}")
+        assert not bool(term.any())
+    env.close()

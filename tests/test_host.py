@@ -264,6 +264,23 @@ def test_bench_byte_models():
             assert r <= n * bench.algorithmic_bytes_per_env_step(U, False, 3)
 
 
+def test_bench_dtype_names_the_state_form():
+    """The bench line's dtype names the UE state form the kernels run (the compact uint8 x4
+    rows on the registered 200 x 200 maps, int16 x4 beyond 255 per side) and the fixed-point
+    reward sum."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    d4, d8 = bench.dtype_string(4), bench.dtype_string(8)
+    assert "uint8x4" in d4 and "int16" not in d4
+    assert "int16x4" in d8 and "uint8" not in d8
+    for d in (d4, d8):
+        assert "fixed-point reward" in d and "f64 rate" in d
+
+
 def test_bench_cpu_baseline_follows_workload():
     """bench.py's cpu_baseline runs the CPU port on the --workload's sizes (shared and per-env
     layouts), one short sample per workload."""

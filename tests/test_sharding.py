@@ -177,3 +177,4 @@ def test_bench_spawns_its_own_ranks():
     assert dd["value_steps_only"] >= out["value"]
     rf = out["roofline"]
     assert "timed region" in rf["launch_ms_basis"] and rf["launch_ms"] > 0
+    assert "uint8x4" in out["dtype"] and "fixed-point reward" in out["dtype"]
