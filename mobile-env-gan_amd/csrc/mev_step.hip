@@ -487,6 +487,7 @@ constexpr int kLdsWaves = MEV_LDS_WAVES;
 constexpr int kLds2Waves = MEV_LDS2_WAVES;
 constexpr int kLds2BytesPerWG = 160 * 1024;
 constexpr int kLds2Window = 3;  // staged rows per window of the two-group rollout (see its launch)
+constexpr int kStage2Bytes = 8;  // bytes per env of a k_steps_lds2 staged row: {isum, nact | done << 7}
 __host__ __device__ constexpr int lds_waves(int ldsm) {
   return ldsm >= 2 ? kLds2Waves : ldsm == 1 ? kLdsWaves : 4;
 }
@@ -1157,7 +1158,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
-  const int nact = ROWS ? __popc(seg_field<PC>(act_w, m)) : __popcll(act_w & segmask);
+  // (every UE active -- registered scenarios: U in the lanes of every env that exists)
+  const int nact = scn_all_active<SCN>() ? U
+                   : ROWS ? __popc(seg_field<PC>(act_w, m)) : __popcll(act_w & segmask);
   // lean path, aligned segments: the utilities (float32 values in [-1, 1]) summed as 2^-25
   // fixed point in int32 -- one DPP add per level instead of two moves and a float64 add;
   // error <= 2^-25 per UE, 1e-8 on the mean, below the float32 reward's own rounding
@@ -1565,8 +1568,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                                           int klead, int row,
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
-                                          int* __restrict__ srow, uint8_t* __restrict__ drow,
-                                          const int* __restrict__ lkeys) {
+                                          int* __restrict__ srow, const int* __restrict__ lkeys) {
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
@@ -1837,7 +1839,8 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     const float rate_f = cf[r] * 0.01f;
     const float util = active[r] ? (float)utility_f32r<SCN>(cf[r], rate_f, kp) : 0.f;
     const int isum = seg_isum_rows<PC>((int)(util * 0x1p25f));  // (util = 0 where inactive)
-    const int nact = __popc(seg_field<PC>(act_w[r], m));
+    // (every UE active -- registered scenarios: the env's count is U in every lane that stores)
+    const int nact = scn_all_active<SCN>() ? U : __popc(seg_field<PC>(act_w[r], m));
     Pending up;
     up.srv = srv[r];
     up.obs = make_float4((float)c[r].pos.x * KPSF(inv_w), (float)c[r].pos.y * KPSF(inv_h),
@@ -1848,16 +1851,16 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     up.e = 0;
     up.reward = 0.f;
     flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
-    // the env's staged row entry: the 2^-25 fixed-point utility sum and {nact, done}; the
-    // workgroup's flush forms the float32 reward from them. Lanes other than the env's last
-    // write into their own histogram word instead (no branch; re-zeroed next step).
+    // the env's staged row entry {the 2^-25 fixed-point utility sum, nact | done << 7}, one
+    // two-word LDS write; the workgroup's flush forms the float32 reward from them. Lanes other
+    // than the env's last write into two words of their env's histogram instead (no branch;
+    // re-zeroed next step; min(): never past the env's area)
     const bool lead = klead < nok[r];
     const int er = r * G + m.seg;
-    int* const hw = h[r] + (HS >= PC ? u : B);
-    int* sw = lead ? srow + er : hw;
-    uint8_t* dw = lead ? drow + er : reinterpret_cast<uint8_t*>(hw);
-    *sw = isum;
-    *dw = (uint8_t)(nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0));
+    int* const hw = h[r] + min(u, PC - 2);
+    int* sw = lead ? srow + 2 * er : hw;
+    sw[0] = isum;
+    sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
     c[r].t += 1;
   }
 }
@@ -2092,8 +2095,7 @@ template <int UC, int SCN, bool TF>
 __device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& out,
                                                const LaneMap& m, const Snap& sn, const EmitF& f,
                                                int e, int nok, int klead, int row,
-                                               int* __restrict__ hist, int* __restrict__ srow,
-                                               uint8_t* __restrict__ drow) {
+                                               int* __restrict__ hist, int* __restrict__ srow) {
   constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
   const int B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
@@ -2114,7 +2116,7 @@ __device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& ou
   const float rate_f = cf * 0.01f;
   const float util = sn.active ? (float)utility_f32r<SCN>(cf, rate_f, kp) : 0.f;
   const int isum = seg_isum_rows<PC>((int)(util * 0x1p25f));
-  const int nact = __popc(seg_field<PC>(sn.act_w, m));
+  const int nact = scn_all_active<SCN>() ? U : __popc(seg_field<PC>(sn.act_w, m));
   Pending up;
   up.srv = srv;
   up.obs = make_float4((float)sn.pos.x * KPSF(inv_w), (float)sn.pos.y * KPSF(inv_h), rate_f, util);
@@ -2125,11 +2127,10 @@ __device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& ou
   up.reward = 0.f;
   flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
   const bool lead = klead < nok;
-  int* const hw = h + (HS >= PC ? u : B);
-  int* sw = lead ? srow + m.seg : hw;
-  uint8_t* dw = lead ? drow + m.seg : reinterpret_cast<uint8_t*>(hw);
-  *sw = isum;
-  *dw = (uint8_t)(nact | ((sn.t + 1 >= KPS(t_end)) ? 0x80 : 0));
+  int* const hw = h + min(u, PC - 2);  // (see lds2_step)
+  int* sw = lead ? srow + 2 * m.seg : hw;
+  sw[0] = isum;
+  sw[1] = nact | ((sn.t + 1 >= KPS(t_end)) ? 0x80 : 0);
 }
 
 // The staged rows of k_steps_lds2: reward = (float)isum 2^-25 / nact (float32, as packed_group's
@@ -2148,20 +2149,21 @@ __device__ __forceinline__ void lds_barrier() {
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
-__device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, const uint8_t* drow,
-                                              int E, int e0, int row0, int nr, float lower,
-                                              int NWG, bool trailing = true) {
+__device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, int E, int e0,
+                                              int row0, int nr, float lower, int NWG,
+                                              bool trailing = true) {
   lds_barrier();
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     const int r = q / NWG, j = q - r * NWG;
     if (e0 + j < E) {
       const size_t ro = (size_t)(row0 + r) * (size_t)E;
       const uint32_t o = (uint32_t)(e0 + j);
-      const uint32_t b = drow[q];
+      const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);  // {isum, nact | done << 7}
+      const uint32_t b = (uint32_t)v.y;
       const int nact = (int)(b & 0x7fu);
       at(out.reward + ro, 4u * o) =
-          nact > 0 ? (float)srow[q] * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
-      at(out.done + ro, o) = (uint8_t)(b >> 7);
+          nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
+      at(out.done + ro, o) = (uint8_t)((b >> 7) & 1u);
     }
   }
   if (trailing) lds_barrier();
@@ -2403,8 +2405,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const int HS = lds2_hist_stride(G, B);
   int* hist = lw + NW * R * G * (8 + KB) + wv * R * G * HS;
   int* ltab = lw + NW * R * G * (8 + KB + HS) + wv * R * G * M;
-  int* srow = lw + NW * R * G * (8 + KB + HS + M);
-  uint8_t* drow = reinterpret_cast<uint8_t*>(srow + stage_rows * NWG);
+  int* srow = lw + NW * R * G * (8 + KB + HS + M);  // staged rows [stage_rows][NWG] int2
   const int npairs = (ngroups + R - 1) / R;  // ("pairs": the wave's R groups)
   const int gstride = (int)gridDim.x * NW;
   const float lower = (float)kp.lower;
@@ -2452,8 +2453,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     const int p = pb + wvu, pn = p + gstride;  // this wave's current / next pair
     const bool cur_ok = p < npairs, nxt_ok = pn < npairs;
     if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pn, f);
-    int* const sw = srow + hb * NWG;
-    uint8_t* const dw = drow + hb * NWG;
+    int* const sw = srow + 2 * hb * NWG;
     const int e0 = pb * G * R;  // the current tile's first env
     if (cur_ok) {
       int e[R], nok[R];
@@ -2472,9 +2472,9 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         do {  // (nsteps >= 1: the loop body runs at least once)
           lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
-              sw + sr * NWG + wvu * G * R, dw + sr * NWG + wvu * G * R, lkeys);
+              sw + 2 * (sr * NWG + wvu * G * R), lkeys);
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-            flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+            flush_staged2(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         } while (i < nsteps);
@@ -2499,9 +2499,9 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         int i = 0, sr = 0;
         auto emit = [&](const Snap& q, const EmitF& ef) {
           pipe_emit_back<UC, SCN, TF>(kp, out, m, q, ef, e[0], nok[0], klead, traj ? i : 0,
-                                      hist, sw + sr * NWG + wvu * G, dw + sr * NWG + wvu * G);
+                                      hist, sw + 2 * (sr * NWG + wvu * G));
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-            flush_staged2(out, sw, dw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+            flush_staged2(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         };
@@ -2568,10 +2568,10 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       MEV_TS(min(4 + 3 * it, 28));
     }
     if (alt) {
-      flush_staged2(out, sw, dw, kp.E, e0, 0, nsteps, lower, NWG, false);
+      flush_staged2(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false);
     } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
       for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-        flush_staged2(out, sw, dw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
+        flush_staged2(out, sw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
                       NWG, true);
     }
     MEV_TS(min(5 + 3 * it, 29));
@@ -3932,7 +3932,7 @@ static int build_lds_tables(mev_ctx* c) {
     total = up16(rate_off + 8 * (size_t)count);
     const int G = kp.envs_per_wave;
     const size_t sh2 = total + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2, true);
-    const size_t row2 = (size_t)kLds2Waves * G * 2 * 5;
+    const size_t row2 = (size_t)kLds2Waves * G * 2 * kStage2Bytes;
     if (sh2 + row2 + 4 > (size_t)kLds2BytesPerWG) return MEV_OK;
     std::vector<double> fullp((size_t)d2max + 1);
     MEV_HIP(hipMemcpy(fullp.data(), c->rate_full, sizeof(double) * fullp.size(),
@@ -4048,7 +4048,7 @@ static int build_lds_tables(mev_ctx* c) {
   if (mode == 3 && (kp.U == 15 || kp.U == 30) && kp.tab_m > 0 && !lds2_off) {
     const int G = kp.envs_per_wave;
     const size_t sh2 = total + kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2);
-    const size_t row2 = (size_t)kLds2Waves * G * 2 * 5;
+    const size_t row2 = (size_t)kLds2Waves * G * 2 * kStage2Bytes;
     if (sh2 + row2 + 4 <= (size_t)kLds2BytesPerWG) {
       c->stage_rows2 = (int)(((size_t)kLds2BytesPerWG - sh2 - 4) / row2);
       if (c->stage_cap > 0) c->stage_rows2 = std::min(c->stage_rows2, c->stage_cap);
@@ -4701,7 +4701,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       const int srows = std::min(c->stage_rows2, nsteps);
       const size_t sh = (size_t)kp.lds_assoc +
                         kLds2Waves * lds2_per_wave(G, kp.B, kp.tab_m, 2, true) +
-                        (((size_t)srows * kLds2Waves * G * 2 * 5 + 3) & ~(size_t)3);
+                        (size_t)srows * kLds2Waves * G * 2 * kStage2Bytes;
       launch_k(k2, dim3(blocks), dim3(64 * kLds2Waves), sh, stream, ev, kp, ks, ko, tb, groups,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
@@ -4762,7 +4762,7 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       // those launches slower (8,192 large envs, pipelined: 270 vs 206 us; 65,536 with two
       // groups per wave and 126 rows: 1.72 vs 1.45 ms), all interleaved on one box.
       const size_t wave_b = (size_t)kp.lds_assoc + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R);
-      const size_t row_b = (size_t)nw2 * G * R * 5;
+      const size_t row_b = (size_t)nw2 * G * R * kStage2Bytes;
       // Two groups per wave: a window of 3 rows. Each flush is a workgroup barrier, and one
       // every 3 steps keeps the workgroup's 16 waves -- adjacent envs -- in step, so their
       // trajectory stores reach the memory together: 168.8 vs 175 us per 20-step and 1.49 vs

@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_ARGS} \
+  timeout -k 10 ${PYTEST_LIMIT:-600} python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_ARGS} \
     > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
