@@ -1547,15 +1547,12 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
   return B + 1 > 64 / G ? B + 1 : 64 / G;
 }
-// A group's context in k_steps_lds2. The per-env flags are bits of one int per lane (the env's
-// value in each of its lanes), changed only inside the wave-uniform draw / reset branch: as
-// per-lane bools the compiler kept them as SGPR lane masks and merged them across every
-// divergent region of the step (three s_andn2 / s_and / s_or per flag and group, every step).
-//   bit 0 (kSok): the env's stream slot holds its stream state (draws past the episode table);
-//   bit 1 (kMov): the env drew past the table in this pair (its state row is stored at the end).
-constexpr int kSok = 1, kMov = 2;
+// A group's context in k_steps_lds2. The env's stream slot (LDS, loaded from its pcg row with
+// the pair) holds its current stream state exactly when drawn > M: an env draws from the
+// episode table while its pair index is below M, and only past it from the stream state, whose
+// last drawing lane writes the slot (mev_restore_stream_state marks restored rows drawn = M + 1).
 struct Ctx2 {
-  int t, drawn, fl;
+  int t, drawn;
   int2 pos, wp;
 };
 
@@ -1634,8 +1631,6 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   for (int r = 0; r < R; ++r) {
     const int er = r * G + m.seg;
     u128* const slot = lpcg + 2 * er;
-    bool fell_back = false;
-    u128 s_fin = 0;
     if (mneed_w[r]) {
       const int k = c[r].drawn + rank[r];
       if ((bal(k >= M) & mneed_w[r]) == 0) {  // every pair precomputed (the common case)
@@ -1643,48 +1638,36 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
           const int p = ltab[er * M + k];
           c[r].wp = make_int2((int)(short)p, p >> 16);
         }
-      } else {  // beyond the table: from the stream state (see packed_group)
-        fell_back = true;
+      } else {
+        // (rare) some lane of the group draws past the episode table: those lanes from the
+        // stream state after the env's pair drawn - 1 -- the table's while drawn <= M, else the
+        // slot's (see Ctx2) -- jumping 2 rank draws ahead (see packed_group); the others from
+        // the table as above
+        const bool past = need[r] && k >= M;
+        if (need[r] && !past) {
+          const int p = ltab[er * M + k];
+          c[r].wp = make_int2((int)(short)p, p >> 16);
+        }
         const u128 inc = slot[1];
-        u128 s;
-        if (!(c[r].fl & kSok) && c[r].drawn > 0) {
+        u128 s = slot[0];
+        if (c[r].drawn > 0 && c[r].drawn <= M) {
           s = at(const_cast<u128*>(tb.tab_st),
-                 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(min(c[r].drawn, M) - 1)));
-          wait_vmem();
-        } else {
-          s = slot[0];
-        }
-        if (reset_env[r]) {  // the state after this episode's U initial pairs
-          s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(U - 1)));
+                 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(c[r].drawn - 1)));
           wait_vmem();
         }
-        if ((bal(rank[r] != 0) & mneed_w[r]) == 0) {
-          if (need[r]) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
+        u128 s_fin = 0;
+        if ((bal(rank[r] != 0) & bal(past)) == 0) {
+          if (past) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
         } else {
-          if (need[r])
+          if (past)
             s_fin = pcg_draw_pair(s, inc, 2 * rank[r], tb.jump, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
         }
         wait_vmem();
+        // the env's last drawing lane keeps the stream state (its env now has drawn > M)
+        if (past && rank[r] == tot[r] - 1) slot[0] = s_fin;
       }
     }
-    // the stream bookkeeping, only where a draw or a reset happened (uniform; without either
-    // nothing changes, and the per-lane masks cost ~15 SALU per group)
-    if (mneed_w[r] | rs_w[r]) {
-      // the slot holds the state after draws past the table (fell_back, uniform); a draw from
-      // the table or a reset leaves it to the table: per env, as lane masks (see Ctx2)
-      const bool tw = tot[r] > 0;
-      int f = c[r].fl;
-      if (fell_back) {
-        const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
-                             (do_reset[r] && tot[r] == 0 && u == U - 1);
-        if (own_fin) slot[0] = s_fin;
-        f = tw ? (f | kSok | kMov) : reset_env[r] ? (f & ~kSok) : f;
-      } else {
-        f = (tw || reset_env[r]) ? (f & ~kSok) : f;
-      }
-      c[r].fl = f;
-      c[r].drawn += tot[r];
-    }
+    c[r].drawn += tot[r];
   }
   // ---- C: movement (movement.py:49-62), branch-free fast path --------------------------------
   // (move_ue_p per lane: arrival snap; axis-parallel moves exactly in float32 when the velocity
@@ -1772,7 +1755,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   } else {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    cell[r] = min((uint32_t)(__mul24(c[r].pos.y, KPS(W)) + c[r].pos.x),
+    cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
                   (uint32_t)(KPS(W) * KPS(H) - 1));
     ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
     full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent[r] & 4095u));
@@ -1960,40 +1943,30 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
   // every draw of the group inside the episode table: the common, branch-free path below;
   // else (rare) every drawing lane from the stream state, as lds2_step's fallback
   const uint64_t fb_w = bal(k >= M) & mneed_w;
-  if (fb_w) {
+  const bool past = need && k >= M;
+  if (fb_w) {  // (rare) lanes drawing past the table: as lds2_step
     u128* const slot = lpcg + 2 * er;
     const u128 inc = slot[1];
-    u128 s;
-    if (!(c.fl & kSok) && c.drawn > 0) {
+    u128 s = slot[0];
+    if (c.drawn > 0 && c.drawn <= M) {
       s = at(const_cast<u128*>(tb.tab_st),
-             16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(min(c.drawn, M) - 1)));
-      wait_vmem();
-    } else {
-      s = slot[0];
-    }
-    if (reset_env) {
-      s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(U - 1)));
+             16u * ((uint32_t)e * (uint32_t)M + (uint32_t)(c.drawn - 1)));
       wait_vmem();
     }
     u128 s_fin = 0;
-    if ((bal(rank != 0) & mneed_w) == 0) {
-      if (need) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
+    if ((bal(rank != 0) & bal(past)) == 0) {
+      if (past) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
     } else {
-      if (need) s_fin = pcg_draw_pair(s, inc, 2 * rank, tb.jump, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
+      if (past) s_fin = pcg_draw_pair(s, inc, 2 * rank, tb.jump, kp.Wd, kp.Hd, c.wp.x, c.wp.y);
     }
     wait_vmem();
-    const bool own_fin = (need && rank == tot - 1) || (do_reset && tot == 0 && u == U - 1);
-    if (own_fin) slot[0] = s_fin;
-    const int fl = c.fl;
-    c.fl = tot > 0 ? (fl | kSok | kMov) : reset_env ? (fl & ~kSok) : fl;
-  } else {
-    c.fl = (tot > 0 || reset_env) ? (c.fl & ~kSok) : c.fl;
+    if (past && rank == tot - 1) slot[0] = s_fin;
   }
   mid();
   if constexpr (!std::is_same_v<std::decay_t<Mid>, PipeNoMid>) __builtin_amdgcn_sched_barrier(0);
   {  // the table's pair (16-lane segments: read a step ahead, pipe_pre), taken where a table
      // draw is due
-    const bool take = need && !fb_w;
+    const bool take = need && !past;
     const int p = PC == 16 ? pre : ltab[er * M + min(k, M - 1)];
     c.wp = take ? make_int2((int)(short)p, p >> 16) : c.wp;
   }
@@ -2051,7 +2024,7 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
 template <int UC, int SCN>
 __device__ __forceinline__ uint32_t pipe_cell(const KParams& kp, const Snap& sn,
                                               const char* __restrict__ lblob) {
-  const uint32_t cell = min((uint32_t)(__mul24(sn.pos.y, KPS(W)) + sn.pos.x),
+  const uint32_t cell = min(__umul24((uint32_t)sn.pos.y, (uint32_t)KPS(W)) + (uint32_t)sn.pos.x,
                             (uint32_t)(KPS(W) * KPS(H) - 1));
   return *reinterpret_cast<const uint16_t*>(lblob + 2u * cell);
 }
@@ -2351,8 +2324,6 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
     const int slot = r * G + m.seg;
     c[r].t = scratch[slot];
     c[r].drawn = scratch[RG + slot];
-    // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
-    c[r].fl = c[r].drawn > M ? kSok : 0;
     if (C8) {
       const int4 q = unpack8((unsigned)f.s8[r]);
       c[r].pos = make_int2(q.x, q.y);
@@ -2548,7 +2519,6 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
                                                 sv_ok ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
         }
-        const bool mvd = (c[r].fl & kMov) != 0;
         const bool ld = env_ok[r] && leader;
         __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].t, out_rsrc(st.t, bt),
                                               ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
@@ -2558,7 +2528,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         const v4u32 sv = {(unsigned)(uint64_t)sl, (unsigned)((uint64_t)sl >> 32),
                           (unsigned)(uint64_t)(sl >> 64), (unsigned)((uint64_t)(sl >> 64) >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(sv, out_rsrc(st.pcg, 12u * bt),
-                                               ld && mvd && (c[r].fl & kSok)
+                                               ld && c[r].drawn > M  // (the slot is current, Ctx2)
                                                    ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
       }
     }
