@@ -2291,15 +2291,18 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
   const int M = KPS(tab_m);
   lds2_pf_wait<R, NT, NK, PE>(f, saturated, C8);
   const int lim = max(1, min(RG * M, (kp.E - p * RG) * M));
+  // Unconditional stores (no branch: the compiler laid guarded ones out of line, past the code
+  // tools/check_prefetch_regs.py scans): a lane past the end writes the slot whose value it
+  // loaded (lds2_prefetch clamps the same way), a duplicate of the same value.
 #pragma unroll
-  for (int q = 0; q < NT; ++q)
-    if (q * 64 + lane < lim) ltab[q * 64 + lane] = f.tab[q];
-  if (lane < 4 * RG) reinterpret_cast<v2u32*>(lpcg)[lane] = f.pc;
-  if (lane < RG) {
-    scratch[lane] = f.t;
-    scratch[RG + lane] = f.d;
+  for (int q = 0; q < NT; ++q) ltab[min(q * 64 + lane, lim - 1)] = f.tab[q];
+  reinterpret_cast<v2u32*>(lpcg)[min(lane >> 2, RG - 1) * 4 + (lane & 3)] = f.pc;
+  {
+    const int j = min(lane, RG - 1);
+    scratch[j] = f.t;
+    scratch[RG + j] = f.d;
     // (the station count: 0 for slots past the batch's last env)
-    if (PE) scratch[2 * RG + lane] = p * RG + lane < kp.E ? (st.bs_count ? f.c : KPS(B)) : 0;
+    if (PE) scratch[2 * RG + j] = p * RG + j < kp.E ? (st.bs_count ? f.c : KPS(B)) : 0;
   }
   __builtin_amdgcn_wave_barrier();
   if (PE) {
