@@ -633,6 +633,8 @@ struct GroupIn {
   bool s_ok;           // fused + draw table: pa holds the state after pair drawn - 1
   int4 s;              // {x, y, wx, wy}
   ulonglong2 pa, pb;   // PCG64 state, increment of the env's movement stream
+  double r100l;        // (one-step TF instances) 100 / lane, correctly rounded: the lane's entry
+                       // of the host's table, read by the lanes through ds_bpermute
 };
 
 template <int SCN = 0>
@@ -642,6 +644,7 @@ __device__ __forceinline__ GroupIn load_group(const KParams& kp, const KState& s
   const int ec = min(e, kp.E - 1);
   GroupIn g;
   const uint32_t ue = (uint32_t)(ec * U + u);
+  g.r100l = 0.0;
   g.t = at(st.t, 4u * (uint32_t)ec);
   g.s = load_ue_at(st.ue_state, ue, KST8);
   if (fused || kp.tab_m) {  // the stream state is read only where a draw needs it (fused:
@@ -1139,9 +1142,20 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   // ---- 4. rate (ResourceFair share, rounded to cents) + utility -----------------------
   double cents = 0.0, rate = 0.0;
   float cents_f = 0.f;
+  double r100b = 0.0;
+  if constexpr (!LDSA && TF) {  // (one-step launches) 100 / n from lane n's table entry (all
+    // lanes active here: ds_bpermute reads the source lanes' registers)
+    const int src = (srv >= 0 ? n : 0) << 2;
+    const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(cur.r100l));
+    const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(cur.r100l));
+    r100b = __hiloint2double(hi, lo);
+  }
   if (srv >= 0) {
     if (LDSA && TF) {  // tie-free table (share_tie_free): the product rounds like the reference
       cents = rint(full * *reinterpret_cast<const double*>(lblob + KPS(lds_r100_off) + 8u * (uint32_t)n));
+      cents_f = (float)cents;
+    } else if (!LDSA && TF) {
+      cents = rint(full * r100b);
       cents_f = (float)cents;
     } else {
       cents = LDSA ? share_cents_r(full, *reinterpret_cast<const double*>(
@@ -1311,7 +1325,9 @@ __device__ __forceinline__ int blob_copy_n16(const KParams& kp, const KTables& t
 
 // Step kernel: one env group per wavefront (latency hidden by occupancy).
 // Groups [g0, ngroups) of the batch (g0 > 0: second half of the two-stream shape).
-template <bool PER_ENV_BS, bool LEAN, int UC, int SCN = 0>
+// TF (scenario instances, share_tie_free, a context with the LDS blob): the share as the
+// product with the host's correctly rounded 100 / n (no reciprocal iterations, no tie test).
+template <bool PER_ENV_BS, bool LEAN, int UC, int SCN = 0, bool TF = false>
 __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState st, KOut out,
                                                              KTables tb, int g0, int ngroups) {
   extern __shared__ int lds_hist[];  // [waves][G][B] when KPS(hist_lds)
@@ -1336,7 +1352,10 @@ __global__ __launch_bounds__(kPackedBlock) void k_step_packed(KParams kp, KState
   const bool env_ok = (m.seg < G) && (e < kp.E);
   if (g < ngroups) {
     GroupIn a = load_group<SCN>(kp, st, tb, e, min(m.u, U - 1), U, false);
-    packed_group<PER_ENV_BS, LEAN, UC, false, 0, SCN, STG>(
+    a.r100l = TF ? *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb.lds_blob) +
+                                                    KPS(lds_r100_off) + 8u * (uint32_t)lane)
+                 : 0.0;
+    packed_group<PER_ENV_BS, LEAN, UC, false, 0, SCN, STG, TF>(
         kp, st, out, tb, m, a, e, env_ok, lds_hist + (threadIdx.x >> 6) * G * kp.B, nullptr,
         nullptr, 0, nullptr, nullptr, srw + (threadIdx.x >> 6) * GC,
         sdn + (threadIdx.x >> 6) * GC);
@@ -4642,10 +4661,12 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
   const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
   StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
-  if (lean && !c->p.bs_per_env && kp.U == 30 && match_scn(c) == 2)  // scenario constants
-    k = k_step_packed<false, true, 30, 2>;
+  // scenario constants; tie-free share with the blob's 100 / n table (k_step_packed TF)
+  const bool tf1 = c->tie_free && c->blob != nullptr;
+  if (lean && !c->p.bs_per_env && kp.U == 30 && match_scn(c) == 2)
+    k = tf1 ? k_step_packed<false, true, 30, 2, true> : k_step_packed<false, true, 30, 2>;
   else if (lean && !c->p.bs_per_env && kp.U == 15 && match_scn(c) == 1)
-    k = k_step_packed<false, true, 15, 1>;
+    k = tf1 ? k_step_packed<false, true, 15, 1, true> : k_step_packed<false, true, 15, 1>;
   const size_t shmem =
       kp.hist_lds ? sizeof(int) * kWavesPerBlock * (size_t)kp.envs_per_wave * kp.B : 0;
   // n > 1 steps on one stream: one launch of the fused multi-step kernel
