@@ -595,8 +595,13 @@ struct LaneMap {
   uint64_t segmask, lt;
 };
 
+// k_steps_lds2's compile-time U may carry kSeg32: UC = kSeg32 + U puts U <= 16 UEs in 32-lane
+// segments (two envs per wavefront instead of four: twice the wavefronts for a small batch)
+constexpr int kSeg32 = 1000;
+__host__ __device__ constexpr int ue_of(int UC) { return UC >= kSeg32 ? UC - kSeg32 : UC; }
 __host__ __device__ constexpr int pitch_of(int U) {
-  return (U > 8 && U <= 16 && 64 / 16 == 64 / U) ? 16
+  return U >= kSeg32 ? 32
+         : (U > 8 && U <= 16 && 64 / 16 == 64 / U) ? 16
          : (U > 16 && U <= 32 && 64 / 32 == 64 / U) ? 32 : U;
 }
 
@@ -1172,9 +1177,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   }
 
   // ---- 5. reward = np.mean(utilities of active UEs, id order) (metrics.py:25-28) ------
-  // (every UE active -- registered scenarios: U in the lanes of every env that exists)
-  const int nact = scn_all_active<SCN>() ? U
-                   : ROWS ? __popc(seg_field<PC>(act_w, m)) : __popcll(act_w & segmask);
+  // (not the constant U of an all-active scenario: the reward's hardware reciprocal of a
+  // constant would be folded at compile time, correctly rounded, one ulp off the other shapes')
+  const int nact = ROWS ? __popc(seg_field<PC>(act_w, m)) : __popcll(act_w & segmask);
   // lean path, aligned segments: the utilities (float32 values in [-1, 1]) summed as 2^-25
   // fixed point in int32 -- one DPP add per level instead of two moves and a float64 add;
   // error <= 2^-25 per UE, 1e-8 on the mean, below the float32 reward's own rounding
@@ -1585,7 +1590,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
                                           int* __restrict__ srow, const int* __restrict__ lkeys) {
-  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  constexpr int PC = pitch_of(UC), U = ue_of(UC), G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
   // lanes UE u of segment s hold valid = u < U; wave masks of the envs that exist (nok[r] of
@@ -1794,7 +1799,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   }
   // per-env histograms in the wave's LDS (bin B: lanes without a station): zero, count, read
   // (16-lane segments of a registered scenario: packed DPP counts instead, row_count_same)
-  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(UC, SCN ? scn_const(SCN).B : 0);
+  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(ue_of(UC), SCN ? scn_const(SCN).B : 0);
   int* h[R];
   int bin[R], n[R];
 #pragma unroll
@@ -1916,7 +1921,7 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
                                           Ctx2& c, int e, int nok, int kval,
                                           u128* __restrict__ lpcg, const int* __restrict__ ltab,
                                           int& pre, Mid&& mid) {
-  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  constexpr int PC = pitch_of(UC), U = ue_of(UC), G = 64 / PC;
   const int M = KPS(tab_m);
   const int u = m.u;
   constexpr uint64_t kValidPat = [] {
@@ -2067,7 +2072,7 @@ __device__ __forceinline__ EmitF pipe_emit_front(const KParams& kp, const LaneMa
   EmitF f;
   f.full = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent & 4095u));
   f.srv = sn.active && ent < 0xF000u ? (int)(ent >> 12) : -1;
-  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(UC, SCN ? scn_const(SCN).B : 0);
+  constexpr bool PCNT = PC == 16 && SCN != 0 && packed_counts_ok(ue_of(UC), SCN ? scn_const(SCN).B : 0);
   int* const h = hist + m.seg * HS;
   if (PCNT) {
     f.n = row_count_same(f.srv);
@@ -2088,7 +2093,7 @@ __device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& ou
                                                const LaneMap& m, const Snap& sn, const EmitF& f,
                                                int e, int nok, int klead, int row,
                                                int* __restrict__ hist, int* __restrict__ srow) {
-  constexpr int PC = pitch_of(UC), U = UC, G = 64 / PC;
+  constexpr int PC = pitch_of(UC), U = ue_of(UC), G = 64 / PC;
   const int B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
   int* const h = hist + m.seg * HS;
@@ -2268,7 +2273,7 @@ template <int UC, int SCN, int R, bool PE, int NT, int NK, bool C8>
 __device__ __forceinline__ void lds2_prefetch(const KParams& kp, const KState& st,
                                               const KTables& tb, const LaneMap& m, int lane,
                                               int p, Pre2<R, NT, NK>& f) {
-  constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC, RG = R * G;
+  constexpr int PC = pitch_of(UC), G = 64 / PC, U = ue_of(UC), RG = R * G;
   const int M = KPS(tab_m);
   const int e0 = p * RG, elast = kp.E - 1;  // the pair's envs [e0, e0 + R G), clamped
 #pragma unroll
@@ -2382,7 +2387,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
   const int NW = (int)(blockDim.x >> 6);  // <= kLds2Waves
-  constexpr int PC = pitch_of(UC), G = 64 / PC, U = UC;
+  constexpr int PC = pitch_of(UC), G = 64 / PC, U = ue_of(UC);
   const int NWG = NW * G * R;  // envs per workgroup tile
   extern __shared__ int lds_all[];
   const char* lblob = reinterpret_cast<const char*>(lds_all);
@@ -4715,18 +4720,28 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // with pairs (or two_groups = 3), registered U = 15 / 30 scenarios whose layout has no cell
     // beyond the mode-3 table's ranks. Measured on one box (200-step launches): 4,096 medium
     // envs 116-118 vs 126 us with the one-group packed kernel; 8,192 large envs 192 vs 252 us.
-    const bool pipe = (tg == 3 || (tg == 0 && !full2)) && (kp.U == 15 || kp.U == 30) &&
+    const bool pipe = (tg == 3 || tg == 4 || (tg == 0 && !full2)) && (kp.U == 15 || kp.U == 30) &&
                       match_scn(c) != 0 && layout_dcount(c) <= 4094;
+    // U = 15 in 32-lane segments (two envs per wavefront, twice the wavefronts) where the
+    // 16-lane form leaves at most one wavefront per SIMD (two_groups = 4 forces it, 3 the
+    // 16-lane form): BASELINE configs[1], 4,096 medium envs, then runs two chains per SIMD
+    const bool seg32 = pipe && kp.U == 15 && tg != 3 &&
+                       (tg == 4 || groups <= c->lds2_wgs * 4);
     if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2) || pipe) &&
-        (tg != 3 || pipe)) {
+        ((tg != 3 && tg != 4) || pipe)) {
       const int R = tg == 1 ? 2 : (tg >= 2 || pipe) ? 1 : 2;
-      const int units = R == 2 ? pairs : groups;  // the waves' work units
+      const int G = seg32 ? 2 : kp.envs_per_wave;  // envs per group
+      const int groups_l = seg32 ? (kp.E + 1) / 2 : groups;
+      const int units = R == 2 ? pairs : groups_l;  // the waves' work units
       const int nw2 = std::max(1, std::min(kLds2Waves, (units + c->lds2_wgs - 1) / c->lds2_wgs));
       const int scn = match_scn(c);
       const bool tf = c->tie_free != 0;  // (scenario instances only)
       StepsKernel k2;
       const bool c8 = kp.st8 != 0;  // (generic instances: the state form as a template flag)
-      if (pipe)
+      if (seg32)
+        k2 = tf ? k_steps_lds2<kSeg32 + 15, 1, false, true, 1, scn_st8(1), true>
+                : k_steps_lds2<kSeg32 + 15, 1, false, false, 1, scn_st8(1), true>;
+      else if (pipe)
         k2 = kp.U == 15 ? (tf ? k_steps_lds2<15, 1, false, true, 1, scn_st8(1), true>
                               : k_steps_lds2<15, 1, false, false, 1, scn_st8(1), true>)
                         : (tf ? k_steps_lds2<30, 2, false, true, 1, scn_st8(2), true>
@@ -4748,7 +4763,6 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                            : c8     ? k_steps_lds2<30, 0, false, false, 1, true>
                                     : k_steps_lds2<30, 0, false, false, 1>);
       const int blocks = std::min((units + nw2 - 1) / nw2, c->lds2_wgs);
-      const int G = kp.envs_per_wave;
       // staged rows: c->stage_rows2 (the count that fits beside 16 waves of two groups), or for
       // one group of 16-lane segments per wave as many as fit beside this launch's waves: 4,096
       // medium envs, 4 waves per workgroup, then flush once per 200-step launch instead of every
@@ -4772,10 +4786,11 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       }
       const int srows = std::max(1, std::min(fit, nsteps));
       const size_t sh = wave_b + (((size_t)srows * row_b + 3) & ~(size_t)3);
-      launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups,
+      launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups_l,
                nsteps, 1, srows);
       MEV_HIP(hipGetLastError());
-      c->last_kind = pipe ? MEV_KIND_LDS2_PIPE : R == 2 ? MEV_KIND_LDS2_TWO : MEV_KIND_LDS2_ONE;
+      c->last_kind = seg32 ? MEV_KIND_LDS2_PIPE32
+                     : pipe ? MEV_KIND_LDS2_PIPE : R == 2 ? MEV_KIND_LDS2_TWO : MEV_KIND_LDS2_ONE;
       return MEV_OK;
     }
     StepsKernel kf = steps_kernel_for(c->p.bs_per_env != 0, lean, ldsm, kp.U);

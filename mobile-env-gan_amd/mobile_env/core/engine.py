@@ -59,7 +59,8 @@ class EngineParams:
     # launch-shape overrides (mev_params; 0 = automatic, results identical for every setting):
     lds_tables: int = 0          # -1 L2 association map, 1..3 that LDS table mode
     two_groups: int = 0          # -1 packed one-group rollouts; 1 / 2 two-group kernel (2 / 1 groups
-                                 # per wave); 3 pipelined one-group kernel (mev.h)
+                                 # per wave); 3 / 4 pipelined one-group kernel, U = 15 in 16- / 32-
+                                 # lane segments (mev.h)
     stage_rows: int = 0          # > 0: at most that many staged per-env rows per window
     xcd_remap: int = 0           # -1 blocks in dispatch order
     scenario_constants: int = 0  # -1 generic kernel instances only
@@ -361,7 +362,8 @@ class StepEngine:
 
     #: mev_last_launch_kind codes (include/mev.h MEV_KIND_*)
     LAUNCH_KINDS = {0: None, 1: "packed_step", 2: "packed_fused", 3: "lds2_two_groups",
-                    4: "lds2_one_group", 5: "lds2_pipelined", 6: "lds2_per_env", 7: "block"}
+                    4: "lds2_one_group", 5: "lds2_pipelined", 6: "lds2_per_env", 7: "block",
+                    8: "lds2_pipelined_seg32"}
 
     @property
     def last_launch_kind(self) -> "str | None":

@@ -2,6 +2,7 @@
 # One GPU session (run from the repo root on the box): STEPS selects the parts, in order --
 #   tests  pytest -m gpu (PYTEST_ARGS, limit PYTEST_LIMIT s) + smoke()
 #   ab     interleaved A/B of libmev_<v>.so variants (VARIANTS, REPS, LENS, WL; tools/ab.sh)
+#   abm    the same at 4,096 medium envs (MVARIANTS, MLENS)
 #   ts     per-wave phase stamps of one TS_LEN-step launch (libmev_ts.so, tools/ts_probe.py)
 #   prof   committed-profile passes (tools/profile.sh) for PROF="tag:args;tag:args"
 #   bench  bench.py lines: the driver's shape (--steps 20 --warmup 5) and the default run
@@ -22,6 +23,9 @@ for s in ${STEPS:-tests}; do
   ab)
     rm -f gpurun_out/ab.log
     bash tools/ab.sh || exit 1 ;;
+  abm)  # medium @ 4,096 (BASELINE configs[1]), appended to the same log
+    WL=mobile-medium-central-v0 E=4096 VARIANTS="${MVARIANTS:-base new}" LENS="${MLENS:-200}" \
+      bash tools/ab.sh || exit 1 ;;
   ts)
     MEV_LIB=$PWD/mobile-env-gan_amd/lib/libmev_ts.so REPS=${TS_REPS:-3} timeout -k 10 120 \
       python tools/ts_probe.py ${TS_LEN:-20} > gpurun_out/ts.log 2>&1 || { echo ts failed; tail gpurun_out/ts.log; exit 1; }
