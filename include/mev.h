@@ -140,8 +140,7 @@ typedef struct mev_params {
    *     1..3 (KTables::lds_blob in mev_step.hip), -1: from the L2 association map;
    *   two_groups: -1: one env group per wavefront in rollout launches (the packed kernel);
    *     0: two groups per wavefront where the batch fills the GPU with pairs, else the
-   *     software-pipelined one-group kernel for the registered U = 15 / 30 scenarios (U = 15 in
-   *     32-lane segments when 16-lane ones would leave at most one wavefront per SIMD), else
+   *     software-pipelined one-group kernel for the registered U = 15 / 30 scenarios, else
    *     the packed kernel; 1 / 2: the two-group kernel with two / one groups per wavefront at
    *     any batch size; 3 / 4: the pipelined one-group kernel at any batch size (where it
    *     applies), U = 15 in 16- / 32-lane segments;
@@ -258,7 +257,7 @@ int mev_rollout_instance(const mev_ctx* ctx);
 #define MEV_KIND_LDS2_PERENV 6   /* fused, per-env layouts, two groups per wavefront */
 #define MEV_KIND_BLOCK 7         /* one workgroup per env (k_steps_block) */
 #define MEV_KIND_LDS2_PIPE32 8   /* the pipelined loop with U <= 16 in 32-lane segments (two envs
-                                    per wavefront: small batches of U = 15) */
+                                    per wavefront; two_groups = 4) */
 int mev_last_launch_kind(const mev_ctx* ctx);
 
 /* 1 when the context's rate table needs no tie test in the ResourceFair share of the kernels

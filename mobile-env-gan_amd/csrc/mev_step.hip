@@ -2878,9 +2878,12 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
                                                       const BlockRow& r, int lane) {
   const double su = wave_sum_f64(lane < nw ? ps[lane] : 0.0);
   if (lane == 63) {
-    const double mean_u = r.nact > 0 ? (su * 0x1p-24) / (double)r.nact : kp.lower;
+    // the float32 reward as the packed kernels' lean path forms it (a float32 product with the
+    // reciprocal; ~1e-7 relative of np.mean), not a float64 division on wave 0's path every step
+    const float mean_u = r.nact > 0 ? (float)su * 0x1p-24f * __builtin_amdgcn_rcpf((float)r.nact)
+                                    : (float)kp.lower;
     const size_t re = (size_t)row * kp.E + e;
-    out.reward[re] = (float)mean_u;
+    out.reward[re] = mean_u;
     out.done[re] = (uint8_t)(r.t_after >= kp.t_end);
   }
 }
@@ -4722,11 +4725,11 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     // envs 116-118 vs 126 us with the one-group packed kernel; 8,192 large envs 192 vs 252 us.
     const bool pipe = (tg == 3 || tg == 4 || (tg == 0 && !full2)) && (kp.U == 15 || kp.U == 30) &&
                       match_scn(c) != 0 && layout_dcount(c) <= 4094;
-    // U = 15 in 32-lane segments (two envs per wavefront, twice the wavefronts) where the
-    // 16-lane form leaves at most one wavefront per SIMD (two_groups = 4 forces it, 3 the
-    // 16-lane form): BASELINE configs[1], 4,096 medium envs, then runs two chains per SIMD
-    const bool seg32 = pipe && kp.U == 15 && tg != 3 &&
-                       (tg == 4 || groups <= c->lds2_wgs * 4);
+    // U = 15 in 32-lane segments (two envs per wavefront, twice the wavefronts; two_groups = 4
+    // only): at 4,096 medium envs two chains per SIMD instead of one, but each with the 32-lane
+    // segments' LDS histogram instead of the packed DPP counts -- 126 vs 101 us per 200-step
+    // launch (interleaved on one box), so the 16-lane form stays the automatic choice
+    const bool seg32 = pipe && kp.U == 15 && tg == 4;
     if (ldsm == 3 && lean && c->lds2_wgs > 0 && pre_ok && (tg > 0 || (tg == 0 && full2) || pipe) &&
         ((tg != 3 && tg != 4) || pipe)) {
       const int R = tg == 1 ? 2 : (tg >= 2 || pipe) ? 1 : 2;

@@ -110,11 +110,11 @@ def test_layout_change_then_pipelined_rollout_vs_oracle():
     eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B), L["bs"], seeds,
                      device="cuda")
     eng.rollout(20)  # one whole episode on the registered layout
-    assert eng.last_launch_kind == "lds2_pipelined_seg32"
+    assert eng.last_launch_kind == "lds2_pipelined"
     new_bs = (np.asarray(L["bs"]) + 7) % 200
     eng.set_bs_layout(torch.as_tensor(new_bs, dtype=torch.int32))
     tr = eng.rollout(45)  # the next episodes: lazy reset, then the new layout throughout
-    assert eng.last_launch_kind in ("lds2_pipelined_seg32", "packed_fused")
+    assert eng.last_launch_kind in ("lds2_pipelined", "packed_fused")
     ob = OracleBatch(OracleParams(), new_bs.tolist(), U, seeds)
     assert_rollout_vs_oracle(tr, ob, 45)
     eng.close()

@@ -8,9 +8,9 @@ assert which kernel ran (``StepEngine.last_launch_kind``, mev_last_launch_kind),
 every step's outputs with the oracle (oracle/vec.py, pinned to the reference's fixtures):
 
 * BASELINE configs[1]: mobile-medium-central-v0 at 4,096 envs -> the software-pipelined
-  one-group rollout with U = 15 in 32-lane segments, velocity 1.5 scenario constants, tie-free
-  share -- every env, 45 steps (two episode resets); and the same batch forced onto the
-  16-lane pipelined kernel and onto the one-group packed kernel;
+  one-group rollout, U = 15 / velocity 1.5 scenario constants, tie-free share -- every env,
+  45 steps (two episode resets); and the same batch forced onto the pipelined kernel with
+  32-lane segments and onto the one-group packed kernel;
 * BASELINE configs[2] (the bench): mobile-large-central-v0 at 65,536 envs -> the two-group
   scenario kernel; every 16th env (4,096 of them) against the oracle run on those envs' seeds
   -- envs are independent, so the subset comparison is exact;
@@ -35,7 +35,7 @@ def _oracle(size, seeds, vel=1.5):
     return OracleBatch(OracleParams(velocity=vel), L["bs"], L["num_ues"], np.asarray(seeds))
 
 
-@pytest.mark.parametrize("two_groups,kind", [(0, "lds2_pipelined_seg32"), (3, "lds2_pipelined"),
+@pytest.mark.parametrize("two_groups,kind", [(0, "lds2_pipelined"), (4, "lds2_pipelined_seg32"),
                                              (-1, "packed_fused")])
 def test_medium_4096_shipped_rollout_vs_oracle(two_groups, kind):
     """BASELINE configs[1] with the kernel make() picks for it (and the packed fallback): one
