@@ -1571,12 +1571,20 @@ __global__ __launch_bounds__(64 * lds_waves(LDSM)) void k_steps_packed(
 __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
   return B + 1 > 64 / G ? B + 1 : 64 / G;
 }
-// A group's context in k_steps_lds2. The env's stream slot (LDS, loaded from its pcg row with
-// the pair) holds its current stream state exactly when drawn > M: an env draws from the
-// episode table while its pair index is below M, and only past it from the stream state, whose
-// last drawing lane writes the slot (mev_restore_stream_state marks restored rows drawn = M + 1).
+// A group's context in k_steps_lds2. The per-env flags are bits of one int per lane (the env's
+// value in each of its lanes), changed only inside the wave-uniform draw / reset branch: as
+// per-lane bools the compiler kept them as SGPR lane masks and merged them across every
+// divergent region of the step (three s_andn2 / s_and / s_or per flag and group, every step).
+//   bit 0 (kSok): the env's stream slot holds its stream state (draws past the episode table);
+//   bit 1 (kMov): the env drew past the table in this pair (its state row is stored at the end).
+// (The pipelined loop, pipe_move, keeps no flags: there the slot is current exactly when
+// drawn > M -- an env draws from the episode table while its pair index is below M, and only
+// past it from the stream state, whose last drawing lane writes the slot; restored rows have
+// drawn = M + 1. Measured: the flag-free form 101 vs 104 us per 200-step launch at 4,096 medium
+// envs, but 1.55 vs 1.51 ms at 65,536 large envs in the two-group loop, interleaved on one box.)
+constexpr int kSok = 1, kMov = 2;
 struct Ctx2 {
-  int t, drawn;
+  int t, drawn, fl;
   int2 pos, wp;
 };
 
@@ -1655,6 +1663,8 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   for (int r = 0; r < R; ++r) {
     const int er = r * G + m.seg;
     u128* const slot = lpcg + 2 * er;
+    bool fell_back = false;
+    u128 s_fin = 0;
     if (mneed_w[r]) {
       const int k = c[r].drawn + rank[r];
       if ((bal(k >= M) & mneed_w[r]) == 0) {  // every pair precomputed (the common case)
@@ -1662,36 +1672,48 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
           const int p = ltab[er * M + k];
           c[r].wp = make_int2((int)(short)p, p >> 16);
         }
-      } else {
-        // (rare) some lane of the group draws past the episode table: those lanes from the
-        // stream state after the env's pair drawn - 1 -- the table's while drawn <= M, else the
-        // slot's (see Ctx2) -- jumping 2 rank draws ahead (see packed_group); the others from
-        // the table as above
-        const bool past = need[r] && k >= M;
-        if (need[r] && !past) {
-          const int p = ltab[er * M + k];
-          c[r].wp = make_int2((int)(short)p, p >> 16);
-        }
+      } else {  // beyond the table: from the stream state (see packed_group)
+        fell_back = true;
         const u128 inc = slot[1];
-        u128 s = slot[0];
-        if (c[r].drawn > 0 && c[r].drawn <= M) {
+        u128 s;
+        if (!(c[r].fl & kSok) && c[r].drawn > 0) {
           s = at(const_cast<u128*>(tb.tab_st),
-                 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(c[r].drawn - 1)));
+                 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(min(c[r].drawn, M) - 1)));
+          wait_vmem();
+        } else {
+          s = slot[0];
+        }
+        if (reset_env[r]) {  // the state after this episode's U initial pairs
+          s = at(const_cast<u128*>(tb.tab_st), 16u * ((uint32_t)e[r] * (uint32_t)M + (uint32_t)(U - 1)));
           wait_vmem();
         }
-        u128 s_fin = 0;
-        if ((bal(rank[r] != 0) & bal(past)) == 0) {
-          if (past) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
+        if ((bal(rank[r] != 0) & mneed_w[r]) == 0) {
+          if (need[r]) s_fin = pcg_draw_pair_next(s, inc, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
         } else {
-          if (past)
+          if (need[r])
             s_fin = pcg_draw_pair(s, inc, 2 * rank[r], tb.jump, kp.Wd, kp.Hd, c[r].wp.x, c[r].wp.y);
         }
         wait_vmem();
-        // the env's last drawing lane keeps the stream state (its env now has drawn > M)
-        if (past && rank[r] == tot[r] - 1) slot[0] = s_fin;
       }
     }
-    c[r].drawn += tot[r];
+    // the stream bookkeeping, only where a draw or a reset happened (uniform; without either
+    // nothing changes, and the per-lane masks cost ~15 SALU per group)
+    if (mneed_w[r] | rs_w[r]) {
+      // the slot holds the state after draws past the table (fell_back, uniform); a draw from
+      // the table or a reset leaves it to the table: per env, as lane masks (see Ctx2)
+      const bool tw = tot[r] > 0;
+      int f = c[r].fl;
+      if (fell_back) {
+        const bool own_fin = (need[r] && rank[r] == tot[r] - 1) ||
+                             (do_reset[r] && tot[r] == 0 && u == U - 1);
+        if (own_fin) slot[0] = s_fin;
+        f = tw ? (f | kSok | kMov) : reset_env[r] ? (f & ~kSok) : f;
+      } else {
+        f = (tw || reset_env[r]) ? (f & ~kSok) : f;
+      }
+      c[r].fl = f;
+      c[r].drawn += tot[r];
+    }
   }
   // ---- C: movement (movement.py:49-62), branch-free fast path --------------------------------
   // (move_ue_p per lane: arrival snap; axis-parallel moves exactly in float32 when the velocity
@@ -1779,7 +1801,11 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   } else {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
+#ifdef MEV_OLD_MUL24
+    cell[r] = min((uint32_t)(__mul24(c[r].pos.y, KPS(W)) + c[r].pos.x),
+#else
     cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
+#endif
                   (uint32_t)(KPS(W) * KPS(H) - 1));
     ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
     full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent[r] & 4095u));
@@ -1864,10 +1890,17 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // re-zeroed next step; min(): never past the env's area)
     const bool lead = klead < nok[r];
     const int er = r * G + m.seg;
+#ifdef MEV_LEAD_BRANCH
+    if (lead) {
+      srow[2 * er] = isum;
+      srow[2 * er + 1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
+    }
+#else
     int* const hw = h[r] + min(u, PC - 2);
     int* sw = lead ? srow + 2 * er : hw;
     sw[0] = isum;
     sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
+#endif
     c[r].t += 1;
   }
 }
@@ -2351,6 +2384,8 @@ __device__ __forceinline__ void lds2_consume(const KParams& kp, const KState& st
     const int slot = r * G + m.seg;
     c[r].t = scratch[slot];
     c[r].drawn = scratch[RG + slot];
+    // the stream slot holds the env's state only after draws past the table (mev_state.pcg)
+    c[r].fl = c[r].drawn > M ? kSok : 0;
     if (C8) {
       const int4 q = unpack8((unsigned)f.s8[r]);
       c[r].pos = make_int2(q.x, q.y);
@@ -2546,6 +2581,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           __builtin_amdgcn_raw_buffer_store_b64(pv, out_rsrc(st.ue_state, bst),
                                                 sv_ok ? 8u * (uint32_t)(e[r] * U + m.u) : bst, 0, 0);
         }
+        // (the slot is current: flags in the two-group loop, drawn > M in the pipelined one)
+        const bool cur_st = PIPE ? c[r].drawn > M : ((c[r].fl & kMov) != 0 && (c[r].fl & kSok) != 0);
         const bool ld = env_ok[r] && leader;
         __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[r].t, out_rsrc(st.t, bt),
                                               ld ? 4u * (uint32_t)e[r] : bt, 0, 0);
@@ -2555,8 +2592,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         const v4u32 sv = {(unsigned)(uint64_t)sl, (unsigned)((uint64_t)sl >> 32),
                           (unsigned)(uint64_t)(sl >> 64), (unsigned)((uint64_t)(sl >> 64) >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(sv, out_rsrc(st.pcg, 12u * bt),
-                                               ld && c[r].drawn > M  // (the slot is current, Ctx2)
-                                                   ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
+                                               ld && cur_st ? 48u * (uint32_t)e[r] : 12u * bt, 0, 0);
       }
     }
     if (nxt_ok) {  // the next pair's inputs (waited for: free after a whole pair's stores)
