@@ -2183,8 +2183,10 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
                                               int row0, int nr, float lower, int NWG,
                                               bool trailing = true) {
   lds_barrier();
+  const float inv_nwg = 1.0f / (float)NWG;
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
-    const int r = q / NWG, j = q - r * NWG;
+    // q / NWG through float (q + 1/2 is >= 1/2 away from a multiple of NWG; exact for q < 2^22)
+    const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
     if (e0 + j < E) {
       const size_t ro = (size_t)(row0 + r) * (size_t)E;
       const uint32_t o = (uint32_t)(e0 + j);
@@ -2473,8 +2475,16 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   // its wait is unconditional -- the trajectory rows of every step, the state's buffer stores
   // below -- so that 2R nsteps + 4R >= 64 of them make the wait free (vmcnt(63)).
   // Staged per-env rows: a pair whose steps fit twice in the window alternates between its two
-  // halves (one barrier per flush), else the window cycles (two).
+  // halves (one barrier per flush), else the window cycles: stage_rows < 0 (the two-group
+  // launches) -- two windows of -stage_rows rows, filled in turn, so that a flush needs only its
+  // leading barrier (the other window is written meanwhile; a window is written again only
+  // after the next flush's barrier, which every reader of its last flush has passed), and a pair
+  // starts in the window after the one its predecessor flushed last; else one window and two
+  // barriers per flush (the trailing one before the window is written again).
+  const bool dbl = stage_rows < 0;
+  if (dbl) stage_rows = -stage_rows;
   const bool alt = 2 * nsteps <= stage_rows;
+  int hcur = 0;  // (dbl) the window being filled
   const bool saturated = 2 * R * nsteps + 4 * R >= 64;  // (2R trajectory stores per step, 4R state)
   int hb = 0;  // the pair's first row slot (alt)
   const bool leader = m.u == PC - 1;
@@ -2488,6 +2498,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     if (nxt_ok) lds2_prefetch<UC, SCN, R, PE, NT, NK, C8>(kp, st, tb, m, lane, pn, f);
     int* const sw = srow + 2 * hb * NWG;
     const int e0 = pb * G * R;  // the current tile's first env
+    const int wrows = stage_rows * NWG;  // (dbl) ints / 2 per window
     if (cur_ok) {
       int e[R], nok[R];
       bool env_ok[R];
@@ -2503,11 +2514,14 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       auto steps = [&](auto full) {
         int i = 0, sr = 0;
         do {  // (nsteps >= 1: the loop body runs at least once)
+          int* const win = sw + (dbl ? 2 * hcur * wrows : 0);
           lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
-              sw + 2 * (sr * NWG + wvu * G * R), lkeys);
-          if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-            flush_staged2(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+              win + 2 * (sr * NWG + wvu * G * R), lkeys);
+          if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps)) {
+            flush_staged2(out, win, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, !dbl);
+            if (dbl) hcur ^= 1;
+          }
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         } while (i < nsteps);
@@ -2603,9 +2617,11 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     if (alt) {
       flush_staged2(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false);
     } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
-      for (int i0 = 0; i0 < nsteps; i0 += stage_rows)
-        flush_staged2(out, sw, kp.E, e0, traj ? i0 : 0, min(stage_rows, nsteps - i0), lower,
-                      NWG, true);
+      for (int i0 = 0; i0 < nsteps; i0 += stage_rows) {
+        flush_staged2(out, sw + (dbl ? 2 * hcur * wrows : 0), kp.E, e0, traj ? i0 : 0,
+                      min(stage_rows, nsteps - i0), lower, NWG, !dbl);
+        if (dbl) hcur ^= 1;
+      }
     }
     MEV_TS(min(5 + 3 * it, 29));
     hb = alt ? nsteps - hb : 0;
@@ -4824,9 +4840,12 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
         if (c->stage_cap > 0) fit = std::min(fit, c->stage_cap);
       }
       const int srows = std::max(1, std::min(fit, nsteps));
-      const size_t sh = wave_b + (((size_t)srows * row_b + 3) & ~(size_t)3);
+      // two groups per wave: two windows of srows rows, one barrier per flush (k_steps_lds2's
+      // stage_rows < 0)
+      const bool dbl = R == 2 && 2 * nsteps > srows && 2 * srows <= c->stage_rows2;
+      const size_t sh = wave_b + (((size_t)(dbl ? 2 : 1) * srows * row_b + 3) & ~(size_t)3);
       launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp, ks, ko, tb, groups_l,
-               nsteps, 1, srows);
+               nsteps, 1, dbl ? -srows : srows);
       MEV_HIP(hipGetLastError());
       c->last_kind = seg32 ? MEV_KIND_LDS2_PIPE32
                      : pipe ? MEV_KIND_LDS2_PIPE : R == 2 ? MEV_KIND_LDS2_TWO : MEV_KIND_LDS2_ONE;
