@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 21
+#define MEV_ABI_VERSION 22
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -143,7 +143,8 @@ typedef struct mev_params {
    *     software-pipelined one-group kernel for the registered U = 15 / 30 scenarios, else
    *     the packed kernel; 1 / 2: the two-group kernel with two / one groups per wavefront at
    *     any batch size; 3 / 4: the pipelined one-group kernel at any batch size (where it
-   *     applies), U = 15 in 16- / 32-lane segments;
+   *     applies), U = 15 in 16- / 32-lane segments. Heterogeneous entities on a shared layout
+   *     (lds_mode 5 tables, when they fit in LDS): 0 / 2 one group per wavefront, 1 two;
    *   stage_rows: > 0: at most that many staged rows of per-env outputs per window;
    *   xcd_remap: -1: blocks in dispatch order (else XCD-contiguous env ranges; 2..8: the
    *     ranges rotated by xcd_remap - 1 XCDs, a placement experiment);
@@ -167,6 +168,12 @@ typedef struct mev_params {
    * (no waypoint) -- half the state bytes, which one-step launches move every step; maps up to
    * 255 per side only (every registered scenario is 200 x 200). 0: int16 [E][U][4]. */
   int32_t compact_state;
+  /* Reward precision. The lean kernels (no float64 outputs) form the float32 reward from
+   * float32 utilities; wherever that sum could miss the reference's float64 mean by more than
+   * 1e-5 relative (mean utilities near zero: cancellation), the env's reward is re-formed from
+   * the exact float64 utilities (reward_risky in mev_step.hip). 1: every reward that way (the
+   * float32 reward of the float64 mean -- slower; tests pin the exact path with it). */
+  int32_t reward_exact;
 } mev_params;
 
 typedef struct mev_state {
@@ -258,6 +265,8 @@ int mev_rollout_instance(const mev_ctx* ctx);
 #define MEV_KIND_BLOCK 7         /* one workgroup per env (k_steps_block) */
 #define MEV_KIND_LDS2_PIPE32 8   /* the pipelined loop with U <= 16 in 32-lane segments (two envs
                                     per wavefront; two_groups = 4) */
+#define MEV_KIND_LDS2_HET 9      /* fused, heterogeneous entities on a shared layout, LDS tables
+                                    (k_steps_lds2 HET) */
 int mev_last_launch_kind(const mev_ctx* ctx);
 
 /* 1 when the context's rate table needs no tie test in the ResourceFair share of the kernels

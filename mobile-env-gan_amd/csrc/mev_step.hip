@@ -74,6 +74,7 @@ struct KParams {
   int srv_bits;       // bits of a serving-BS index (ceil(log2(B))), for the ballot match
   int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
   int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
+  float u_err;        // bound on |float32 utility (utility_f32r) - float64 utility| (reward_risky)
   int hist_lds;       // packed shape: per-env BS counts in an LDS histogram ([G][B] per wave)
   int tab_m;          // episode draw table: pairs per env (0: off)
   float inv_w, inv_h; // obs normalisation
@@ -548,6 +549,55 @@ __device__ __forceinline__ int seg_isum_rows(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
   if (P == 32) x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, true);
+  return x;
+}
+
+// ---- Reward exactness guard --------------------------------------------------------------------
+// north_star holds the float32 reward to 1e-5 relative of the reference's float64 mean utility
+// (metrics.py:25-28). The lean kernels sum float32 utilities, each within kp.u_err of the
+// float64 value (the host's bound for the utility parameters), as fixed point (quantum q per
+// UE); that mean is within 1e-5 unless the sum is small against its error bound --
+// nact (u_err + q) >= 9.5e-6 |sum|: mean utilities near zero, cancellation (none in the
+// registered large / medium / mixed workloads; ~1 % of small's env-steps). Such an env's reward
+// comes from the exact float64 utilities (the device table tb.util by cents, utility_of) summed
+// as 2^-50 fixed point in int64: associative, so every kernel shape forms the same bits.
+__device__ __forceinline__ bool reward_risky(float sum, int nact, float q, const KParams& kp) {
+  return nact > 0 && fabsf(sum) * 9.5e-6f <= (float)nact * (kp.u_err + q);
+}
+__device__ __forceinline__ long long util_fix50(double cents, bool take, const KParams& kp,
+                                                const double* __restrict__ tab) {
+  if (!take) return 0;
+  const double uu = cents <= (double)kp.util_kmax ? tab[(int)cents] : kp.util_sat;
+  return (long long)(uu * 0x1p50);
+}
+__device__ __forceinline__ float exact_mean50(long long s, int nact) {
+  return (float)((double)s * 0x1p-50 / (double)nact);
+}
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ long long dpp_i64(long long v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(unsigned long long)v, CTRL, ROWMASK, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((unsigned long long)v >> 32), CTRL,
+                                             ROWMASK, 0xf, true);
+  return (long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// int64 sum over an aligned segment of P = 16 / 32 / 64 lanes (all lanes active), valid in the
+// segment's last lane (seg_sum_rows' pattern; P = 64: + row_bcast:31 into rows 2 and 3)
+template <int P>
+__device__ __forceinline__ long long seg_lsum_rows(long long x) {
+  x += dpp_i64<0x111>(x);
+  x += dpp_i64<0x112>(x);
+  x += dpp_i64<0x114>(x);
+  x += dpp_i64<0x118>(x);
+  if (P >= 32) x += dpp_i64<0x142, 0xa>(x);
+  if (P == 64) x += dpp_i64<0x143, 0xc>(x);
+  return x;
+}
+// ... over U consecutive lanes (seg_sum's pattern), valid in the segment's first lane
+__device__ __forceinline__ long long seg_lsum(long long x, int U, int u) {
+  for (int off = 1; off < U; off <<= 1) {
+    const long long y = __shfl_down(x, (unsigned)off);
+    if (u + off < U) x += y;
+  }
   return x;
 }
 
@@ -1187,6 +1237,20 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   const double sum_u = ISUM ? 0.0
                             : ROWS ? seg_sum_rows<PC>(util, active) : seg_sum(util, active, U, u);
   const int isum_u = ISUM ? seg_isum_rows<PC>(active ? (int)((float)util * 0x1p25f) : 0) : 0;
+  // reward_risky (rare): the env's mean from the exact utilities
+  bool use_exact = false;
+  float exact_r = 0.f;
+  if constexpr (LEAN) {
+    const bool risky = env_ok && leader &&
+                       reward_risky(ISUM ? (float)isum_u * 0x1p-25f : (float)sum_u, nact,
+                                    ISUM ? 0x1p-25f : 0.f, kp);
+    if (bal(risky)) {
+      const long long v = util_fix50(cents, active, kp, tb.util);
+      const long long se = ROWS ? seg_lsum_rows<PC>(v) : seg_lsum(v, U, u);
+      use_exact = risky;
+      exact_r = exact_mean50(se, nact);
+    }
+  }
   double sum_r = 0.0;
   if (want_metrics)
     sum_r = ROWS ? seg_sum_rows<PC>(rate, srv >= 0) : seg_sum(rate, srv >= 0, U, u);
@@ -1241,7 +1305,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
         : LEAN ? (nact > 0 ? (double)((float)sum_u * __builtin_amdgcn_rcpf((float)nact))
                            : kp.lower)
                : (nact > 0 ? sum_u / (double)nact : kp.lower);
-    reward_out = (float)mean_u;
+    reward_out = use_exact ? exact_r : (float)mean_u;
     if (want_metrics) {
       const int ncon = __popcll(mcon);
       const double mean_r = ncon > 0 ? sum_r / (double)ncon : 0.0;
@@ -1590,14 +1654,20 @@ struct Ctx2 {
 
 // FULL: every env of both groups exists (all pairs but the batch's last partial one): the
 // env / valid lane masks are constants, no per-step mask arithmetic.
-template <int UC, int SCN, int R, bool PE, bool TF = false, bool FULL = false>
+// HET: heterogeneous entities with a shared layout (KParams::lds_mode 5, build_het_lds): the
+// lane's UE class hcu and movement parameters hmv (per UE, tb.mv); the association from the
+// LDS cell map of the closest station within any pair's reach, s*, which serves the UE when the
+// (class of s*, UE class) pair connects at that distance -- the closest station overall is then
+// the closest connectable one, ties by index included -- else from the UE class's L2 map.
+template <int UC, int SCN, int R, bool PE, bool TF = false, bool FULL = false, bool HET = false>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
                                           const int (&e)[R], const int (&nok)[R], int kval,
                                           int klead, int row,
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
-                                          int* __restrict__ srow, const int* __restrict__ lkeys) {
+                                          int* __restrict__ srow, const int* __restrict__ lkeys,
+                                          int hcu = 0, const MoveP& hmv = MoveP{}) {
   constexpr int PC = pitch_of(UC), U = ue_of(UC), G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
@@ -1722,8 +1792,17 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   constexpr bool V15 = scn_v15<SCN>();  // velocity 1.5 in integers (step_v15)
   int2 npos[R];
   bool arrive[R];
+  if constexpr (HET) {  // each UE with its own velocity: move_ue_p with the lane's parameters
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < R; ++r) {
+      int2 p = c[r].pos, w = c[r].wp;
+      if (active[r]) move_ue_p(p, w, hmv);
+      c[r].pos = p;
+      c[r].wp = w;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R && !HET; ++r) {
     const int2 pos = c[r].pos, wp = c[r].wp;
     const int dx = wp.x - pos.x, dy = wp.y - pos.y;
     const int ax2 = __mul24(dx, dx), ay2 = __mul24(dy, dy);
@@ -1757,7 +1836,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     npos[r] = arrive[r] ? wp : np;
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) {  // selects (an `if` here became an exec-mask branch)
+  for (int r = 0; r < R && !HET; ++r) {  // selects (an `if` here became an exec-mask branch)
     const bool pop = active[r] && arrive[r];
     c[r].pos = active[r] ? npos[r] : c[r].pos;
     c[r].wp = pop ? make_int2(-1, -1) : c[r].wp;
@@ -1798,14 +1877,41 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
       cell[r] = ent[r] = 0;
     }
+  } else if (HET) {
+    // {s*, rank k of d2 in D of s*'s class} per cell; per (UE class, station): {the offset of
+    // the pair's rates over that D, the pair's largest connectable rank}
+    const int cells = KPS(W) * KPS(H);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
+                    (uint32_t)(cells - 1));
+      ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
+      const bool has = ent[r] < 0xF000u;
+      const uint32_t s = has ? ent[r] >> 12 : 0u, k = has ? ent[r] & 4095u : 0u;
+      const int2 pk = *reinterpret_cast<const int2*>(lblob + kp.lds_st_off +
+                                                     8u * ((uint32_t)hcu * (uint32_t)B + s));
+      const bool conn = has && (int)k <= pk.y;
+      full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) +
+                                                 8u * (conn ? (uint32_t)pk.x + k : 0u));
+      srv[r] = active[r] && conn ? (int)s : -1;
+      // s* out of this class's reach (another station may serve it), or a rank past the
+      // table: the class's L2 map (rare, uniform branch; its load waited for inside)
+      const bool fb = active[r] && ((has && !conn) || ent[r] == 0xFFFFu);
+      if (bal(fb) & act_w[r]) {
+        if (fb) {
+          const int4 q = at(const_cast<int4*>(tb.assoc),
+                            16u * ((uint32_t)hcu * (uint32_t)cells + cell[r]));
+          srv[r] = q.x;
+          full[r] = __hiloint2double(q.w, q.z);
+        }
+        wait_vmem();
+      }
+      ent[r] = 0;  // (the far-cell path below is this one's)
+    }
   } else {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-#ifdef MEV_OLD_MUL24
-    cell[r] = min((uint32_t)(__mul24(c[r].pos.y, KPS(W)) + c[r].pos.x),
-#else
     cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
-#endif
                   (uint32_t)(KPS(W) * KPS(H) - 1));
     ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
     full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * (ent[r] & 4095u));
@@ -1814,7 +1920,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    if (!PE && (bal(ent[r] == 0xFFFFu) & act_w[r])) {  // cells beyond the table's ranks: L2 map
+    if (!PE && !HET && (bal(ent[r] == 0xFFFFu) & act_w[r])) {  // cells beyond the table's ranks: L2 map
       if (active[r] && ent[r] == 0xFFFFu) {
         const int4 q = at(const_cast<int4*>(tb.assoc), 16u * cell[r]);
         srv[r] = q.x;
@@ -1889,18 +1995,21 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // than the env's last write into two words of their env's histogram instead (no branch;
     // re-zeroed next step; min(): never past the env's area)
     const bool lead = klead < nok[r];
-    const int er = r * G + m.seg;
-#ifdef MEV_LEAD_BRANCH
-    if (lead) {
-      srow[2 * er] = isum;
-      srow[2 * er + 1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
+    // (reward_risky, rare: the exact reward's float32 bits instead, flag 0x100)
+    const bool risky = lead && reward_risky((float)isum * 0x1p-25f, nact, 0x1p-25f, kp);
+    int word0 = isum, flag = 0;
+    if (bal(risky)) {
+      const long long se = seg_lsum_rows<PC>(util_fix50((double)cf[r], active[r], kp, tb.util));
+      if (risky) {
+        word0 = __float_as_int(exact_mean50(se, nact));
+        flag = 0x100;
+      }
     }
-#else
+    const int er = r * G + m.seg;
     int* const hw = h[r] + min(u, PC - 2);
     int* sw = lead ? srow + 2 * er : hw;
-    sw[0] = isum;
-    sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
-#endif
+    sw[0] = word0;
+    sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0) | flag;
     c[r].t += 1;
   }
 }
@@ -2157,6 +2266,8 @@ __device__ __forceinline__ void pipe_emit_back(const KParams& kp, const KOut& ou
   up.reward = 0.f;
   flush_pending<true, false>(out, up, (uint32_t)kp.E, (uint32_t)(kp.E * U), (uint32_t)row);
   const bool lead = klead < nok;
+  // (reward_risky: tested by the flush, flush_staged2<true> -- a branch here, on the pipelined
+  // loop's path, cost 9 % at 4,096 medium envs)
   int* const hw = h + min(u, PC - 2);  // (see lds2_step)
   int* sw = lead ? srow + 2 * m.seg : hw;
   sw[0] = isum;
@@ -2179,23 +2290,57 @@ __device__ __forceinline__ void lds_barrier() {
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
+// DETECT (the pipelined loop, whose steps do not test reward_risky): the flush tests every row's
+// fixed-point sum, and if any row of the workgroup's window is risky (block-uniform, one
+// __syncthreads_or per flush) re-forms those rows' rewards from the exact utilities of the
+// window's obs rates (every wave's stores made visible by a fenced barrier first; cents =
+// rint(100 rate) exactly below 6e6, every table index is below 2^22; the env's UEs are all
+// active or none, nact = U or 0). U: UEs per env.
+template <bool DETECT = false>
 __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, int E, int e0,
                                               int row0, int nr, float lower, int NWG,
-                                              bool trailing = true) {
+                                              bool trailing = true, const KParams* kp = nullptr,
+                                              const double* utab = nullptr, int U = 0) {
   lds_barrier();
   const float inv_nwg = 1.0f / (float)NWG;
+  bool any = false;
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     // q / NWG through float (q + 1/2 is >= 1/2 away from a multiple of NWG; exact for q < 2^22)
     const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
     if (e0 + j < E) {
       const size_t ro = (size_t)(row0 + r) * (size_t)E;
       const uint32_t o = (uint32_t)(e0 + j);
-      const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);  // {isum, nact | done << 7}
+      // {isum, nact | done << 7}, or {the exact reward's bits, ... | 0x100} (reward_risky)
+      const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
       const uint32_t b = (uint32_t)v.y;
       const int nact = (int)(b & 0x7fu);
       at(out.reward + ro, 4u * o) =
-          nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
+          (b & 0x100u) ? __int_as_float(v.x)
+                       : nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
       at(out.done + ro, o) = (uint8_t)((b >> 7) & 1u);
+      if (DETECT) any = any || (!(b & 0x100u) && reward_risky((float)v.x * 0x1p-25f, nact, 0x1p-25f, *kp));
+    }
+  }
+  if (DETECT && __syncthreads_or(any)) {  // rare
+    __syncthreads();  // (fenced: the window's obs stores of every wave visible)
+    // (rolled loops, the pointers laundered inside the branch: inlined into the step loop, an
+    // unrolled fix-up held ~20 VGPRs across it)
+    const float* obs_f = reinterpret_cast<const float*>(out.obs);
+    float* rew = out.reward;
+    asm volatile("" : "+s"(obs_f), "+s"(rew), "+s"(utab));
+#pragma unroll 1
+    for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
+      const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
+      if (e0 + j >= E) continue;
+      const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
+      const uint32_t b = (uint32_t)v.y;
+      const int nact = (int)(b & 0x7fu);
+      if ((b & 0x100u) || !reward_risky((float)v.x * 0x1p-25f, nact, 0x1p-25f, *kp)) continue;
+      const float* rates = obs_f + 4 * ((size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)) * (size_t)U + 2;
+      long long su = 0;
+#pragma unroll 1
+      for (int u = 0; u < U; ++u) su += util_fix50(rint((double)rates[4 * u] * 100.0), true, *kp, utab);
+      rew[(size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)] = exact_mean50(su, nact);
     }
   }
   if (trailing) lds_barrier();
@@ -2418,8 +2563,9 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 // prefetch registers of one form only: a runtime choice kept both sets live, and spilled them)
 // PIPE: the software-pipelined step loop (pipe_move / pipe_emit; R = 1, shared layout, a layout
 // without cells beyond the mode-3 table's ranks)
+// HET: heterogeneous entities, shared layout (lds2_step's HET; the generic instance only)
 template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2, bool C8 = scn_st8(SCN),
-          bool PIPE = false>
+          bool PIPE = false, bool HET = false>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -2445,6 +2591,10 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const int gstride = (int)gridDim.x * NW;
   const float lower = (float)kp.lower;
   const int pb0 = block_slot(kp.xcd_remap) * NW;
+  static_assert(!HET || (SCN == 0 && !PE && !PIPE), "HET: the generic shared-layout instance");
+  // (HET) this lane's UE class and movement parameters, for the launch
+  const int hcu = HET ? (int)tb.ue_cls[min(m.u, U - 1)] : 0;
+  const MoveP hmv = HET ? tb.mv[min(m.u, U - 1)] : MoveP{};
   constexpr int NT = lds2_pre_words<UC, SCN, R>();
   constexpr int NK = PE ? (R * G * 16 + 63) / 64 : 1;
   Pre2<R, NT, NK> f;  // the inputs of the wave's next pair
@@ -2515,9 +2665,9 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         int i = 0, sr = 0;
         do {  // (nsteps >= 1: the loop body runs at least once)
           int* const win = sw + (dbl ? 2 * hcur * wrows : 0);
-          lds2_step<UC, SCN, R, PE, TF, decltype(full)::value>(
+          lds2_step<UC, SCN, R, PE, TF, decltype(full)::value, HET>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
-              win + 2 * (sr * NWG + wvu * G * R), lkeys);
+              win + 2 * (sr * NWG + wvu * G * R), lkeys, hcu, hmv);
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps)) {
             flush_staged2(out, win, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, !dbl);
             if (dbl) hcur ^= 1;
@@ -2548,7 +2698,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           pipe_emit_back<UC, SCN, TF>(kp, out, m, q, ef, e[0], nok[0], klead, traj ? i : 0,
                                       hist, sw + 2 * (sr * NWG + wvu * G));
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-            flush_staged2(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true);
+            flush_staged2<true>(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true, &kp,
+                                tb.util, U);
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         };
@@ -2615,11 +2766,12 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       MEV_TS(min(4 + 3 * it, 28));
     }
     if (alt) {
-      flush_staged2(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false);
-    } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only
+      flush_staged2<PIPE>(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false, &kp, tb.util, U);
+    } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only (the same
+                           // barriers as the waves with pairs: DETECT as theirs)
       for (int i0 = 0; i0 < nsteps; i0 += stage_rows) {
-        flush_staged2(out, sw + (dbl ? 2 * hcur * wrows : 0), kp.E, e0, traj ? i0 : 0,
-                      min(stage_rows, nsteps - i0), lower, NWG, !dbl);
+        flush_staged2<PIPE>(out, sw + (dbl ? 2 * hcur * wrows : 0), kp.E, e0, traj ? i0 : 0,
+                            min(stage_rows, nsteps - i0), lower, NWG, !dbl, &kp, tb.util, U);
         if (dbl) hcur ^= 1;
       }
     }
@@ -2927,12 +3079,31 @@ __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& 
 // 2^53, any order) instead of one lane's chain of dependent LDS reads; lane 63 writes.
 __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const KOut& out,
                                                       const double* ps, int nw, int e, int row,
-                                                      const BlockRow& r, int lane) {
+                                                      const BlockRow& r, int lane, bool fix,
+                                                      const double* __restrict__ utab) {
   const double su = wave_sum_f64(lane < nw ? ps[lane] : 0.0);
+  // reward_risky (rare, wave-uniform): the exact mean from the row's obs rates, which every wave
+  // stored before the barrier this one follows (fenced: __syncthreads); `fix`: the row is still
+  // there (trajectory rows, or the launch's last row). cents = rint(100 rate) exactly below 6e6,
+  // every table index is below 2^22; the env's UEs are all active or none (nact = U or 0).
+  float exact = 0.f;
+  const float sum_f = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                    __builtin_bit_cast(int, (float)su), 63));
+  const bool risky = fix && reward_risky(sum_f * 0x1p-24f, r.nact, 0x1p-24f, kp);
+  if (risky) {  // (rolled, the pointers laundered inside the branch: see flush_staged2)
+    const float* obs_f = reinterpret_cast<const float*>(out.obs);
+    asm volatile("" : "+s"(obs_f), "+s"(utab));
+    const float* rates = obs_f + 4 * ((size_t)row * kp.E + (size_t)e) * (size_t)kp.U + 2;
+    long long v = 0;
+#pragma unroll 1
+    for (int u = lane; u < kp.U; u += 64) v += util_fix50(rint((double)rates[4 * u] * 100.0), true, kp, utab);
+    exact = exact_mean50(seg_lsum_rows<64>(v), r.nact);
+  }
   if (lane == 63) {
     // the float32 reward as the packed kernels' lean path forms it (a float32 product with the
     // reciprocal; ~1e-7 relative of np.mean), not a float64 division on wave 0's path every step
-    const float mean_u = r.nact > 0 ? (float)su * 0x1p-24f * __builtin_amdgcn_rcpf((float)r.nact)
+    const float mean_u = risky ? exact
+                       : r.nact > 0 ? (float)su * 0x1p-24f * __builtin_amdgcn_rcpf((float)r.nact)
                                     : (float)kp.lower;
     const size_t re = (size_t)row * kp.E + e;
     out.reward[re] = mean_u;
@@ -3422,7 +3593,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // step's barrier)
       if (LEAN ? (w == 0 && i > 0) : (tid == 0 && i > 0)) {
         const double* pps = L.ps + 64 * (par ^ 1);
-        if (LEAN) block_finish_row_lean(kp, out, pps, nv, e, traj ? i - 1 : 0, prev, lane);
+        if (LEAN) block_finish_row_lean(kp, out, pps, nv, e, traj ? i - 1 : 0, prev, lane, traj != 0, tb.util);
         else block_finish_row<LEAN>(kp, out, pps, L.wt + 64 * (par ^ 1), nv, e, traj ? i - 1 : 0, prev);
       }
       prev = BlockRow{t + 1, nact, ncon};
@@ -3433,7 +3604,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     __syncthreads();  // the last step's partial sums
     if (LEAN ? (w == 0 && nsteps > 0) : (tid == 0 && nsteps > 0)) {
       const int lp = (nsteps - 1) & 1;  // the last step's parity
-      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev, lane);
+      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev, lane, true, tb.util);
       else block_finish_row<LEAN>(kp, out, L.ps + 64 * lp, L.wt + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev);
     }
     // ---- epilogue: the state after the last step ----------------------------------------
@@ -3668,6 +3839,105 @@ __global__ void k_lds_map3(const int4* __restrict__ map, int cells, const uint2*
   }
 }
 
+// Heterogeneous entities with a shared layout, LDS form (KParams::lds_mode 5, the two-group
+// rollout's HET instances), built per layout on the device:
+//   k_het_cells: per cell the closest station s* within `reach` (the largest pair d2max; ties to
+//     the lower index) and its squared distance, flagged in the set D_cb of its station class cb;
+//   k_d2_prefix (per class): the rank index of each D_cb;
+//   k_het_info: T = sum |D_cb|, the class bases, and per (UE class cu, station j) the pair's
+//     rate offset cu T + base_cb(j) and its largest connectable rank (d2 <= the pair's d2max);
+//   k_het_map: the u16 cell entries (s* << 12 | rank of d2 in D_cb; 0xF000 nothing in reach,
+//     0xFFFF rank past 4,094) and the rates [cu][cb][k] of every pair over D_cb.
+__global__ void k_het_cells(const int2* __restrict__ bs, int B, int W, int H, int reach,
+                            const uint8_t* __restrict__ bs_cls, int2* __restrict__ cellv,
+                            uint8_t* __restrict__ flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * H) return;
+  const int x = i % W, y = i / W;
+  long long best = LLONG_MAX;
+  int jb = -1;
+  for (int j = 0; j < B; ++j) {
+    const int2 q = bs[j];
+    const long long dx = (long long)x - q.x, dy = (long long)y - q.y;
+    const long long d2 = dx * dx + dy * dy;
+    if (d2 < best) {
+      best = d2;
+      jb = j;
+    }
+  }
+  if (jb >= 0 && best <= reach) {
+    cellv[i] = make_int2(jb, (int)best);
+    flag[(size_t)bs_cls[jb] * (size_t)(reach + 1) + (size_t)best] = 1;
+  } else {
+    cellv[i] = make_int2(-1, 0);
+  }
+}
+
+// rank of d2 in D_cb (d2 <= reach) from its rank index; d2 = reach + 1: |D_cb|
+__device__ __forceinline__ uint32_t het_rank(const uint2* __restrict__ words, int nwords, uint32_t d2,
+                                             uint32_t reach) {
+  if (d2 > reach) return words[nwords].x;
+  const uint2 w = words[d2 >> 5];
+  return w.y + (uint32_t)__popc(w.x & ((1u << (d2 & 31u)) - 1u));
+}
+
+// info: [0] the rates a copy needs (the sum of the pairs' runs), [2 + cb NU + cu] the offset of
+// pair (cb, cu)'s run of rates, [2 + NB NU + cb NU + cu] its largest connectable rank (-1: none);
+// and per (UE class cu, station j) the pair's {offset, largest rank} into the blob at pk
+__global__ void k_het_info(const uint2* __restrict__ words, int nwords, int NB, int NU, int B,
+                           const uint8_t* __restrict__ bs_cls, const int2* __restrict__ pair,
+                           int reach, int2* __restrict__ pk, int* __restrict__ info) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int off = 0;
+  for (int cu = 0; cu < NU; ++cu)
+    for (int cb = 0; cb < NB; ++cb) {
+      const int dmx = pair[cb * NU + cu].y;  // (-1: the pair never connects)
+      const uint2* w = words + (size_t)cb * (nwords + 1);
+      const int kmax = dmx < 0 ? -1
+                                : (int)het_rank(w, nwords, (uint32_t)min(dmx, reach) + 1u, (uint32_t)reach) - 1;
+      info[2 + cb * NU + cu] = off;
+      info[2 + NB * NU + cb * NU + cu] = kmax;
+      off += min(kmax + 1, (int)kLds3Rates - 1);
+    }
+  info[0] = off;
+  for (int cu = 0; cu < NU; ++cu)
+    for (int j = 0; j < B; ++j) {
+      const int q = (int)bs_cls[j] * NU + cu;
+      pk[cu * B + j] = make_int2(info[2 + q], info[2 + NB * NU + q]);
+    }
+}
+
+__global__ void k_het_map(const int2* __restrict__ cellv, int cells, const uint2* __restrict__ words,
+                          int nwords, int reach, int NB, int NU, const uint8_t* __restrict__ bs_cls,
+                          const int2* __restrict__ pair, const double* __restrict__ rate_full,
+                          const int* __restrict__ info, uint8_t* __restrict__ blob, int rate_off,
+                          int rate_cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cells) {
+    const int2 v = cellv[i];
+    uint32_t ent = 0xF000u;  // nothing within any pair's reach
+    if (v.x >= 0) {
+      const uint32_t k = het_rank(words + (size_t)bs_cls[v.x] * (nwords + 1), nwords, (uint32_t)v.y,
+                                  (uint32_t)reach);
+      ent = k < kLds3Rates - 1 ? ((uint32_t)v.x << 12) | k : 0xFFFFu;
+    }
+    reinterpret_cast<uint16_t*>(blob)[i] = (uint16_t)ent;
+  }
+  const int nd = reach + 1;
+  if (i < NB * nd) {
+    const int cb = i / nd, d = i - cb * nd;
+    const uint2* w = words + (size_t)cb * (nwords + 1);
+    if ((w[(uint32_t)d >> 5].x >> (d & 31)) & 1u) {
+      const int k = (int)het_rank(w, nwords, (uint32_t)d, (uint32_t)reach);
+      for (int cu = 0; cu < NU; ++cu) {
+        const int q = cb * NU + cu, at_k = info[2 + q] + k;
+        if (k <= info[2 + NB * NU + q] && k < (int)kLds3Rates - 1 && at_k < rate_cap)
+          reinterpret_cast<double*>(blob + rate_off)[at_k] = rate_full[pair[q].x + d];
+      }
+    }
+  }
+}
+
 // Episode draw table of the envs with mask[e] (all if NULL): pair k of env e = draws 2k and
 // 2k + 1 of the stream re-seeded to state0 (what every episode of the env draws, in order),
 // and the stream state after them. One thread per (env, pair).
@@ -3784,6 +4054,18 @@ struct mev_ctx {
   MoveP* h_mv;
   int16_t* h_perm;
   int* h_seg;
+  // heterogeneous entities on the two-group rollout: KParams::lds_mode 5 tables of the shared
+  // layout (mev_update_stations: k_het_cells / k_d2_prefix / k_het_info / k_het_map; their
+  // rate count read back like mode 3's |D|, through dcount_pin); het_lds 0: packed kernels only
+  int het_lds;
+  int het_reach, het_nwords, het_r100_off, het_st_off, het_rate_off, het_rate_cap, het_cus;
+  int2* het_cell;
+  uint8_t* het_flag;
+  uint2* het_words;
+  int* het_info;
+  uint8_t* het_blob;
+  mutable size_t het_occ_key;  // (the launch shape het_occ_n was computed for)
+  mutable int het_occ_n;
 };
 
 static thread_local char g_hip_err[256] = "";
@@ -4277,6 +4559,52 @@ static int build_het(mev_ctx* c) {
   return MEV_OK;
 }
 
+// The two-group rollout's tables for heterogeneous entities with a shared layout (lds_mode 5),
+// allocated here and filled per layout by mev_update_stations. Blob: [0, 2 cells) the u16 cell
+// entries, [r100_off, +576) 100 / n, [st_off, +8 NU B) the {offset, largest rank} of each (UE
+// class, station) pair, [rate_off, ...) the pairs' runs of rates. Eligible: U = 15 / 30, at most
+// 15 stations (4-bit station field), a draw table, cells < 65,536 rounded into LDS beside at least
+// one wavefront; two_groups >= 0 and lds_tables >= 0.
+static int build_het_lds(mev_ctx* c) {
+  const KParams& kp = c->kp;
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  c->het_lds = 0;
+  const size_t cells = (size_t)c->p.width * c->p.height;
+  if (!c->het_packed || c->p.two_groups < 0 || c->p.lds_tables < 0 || !(kp.U == 15 || kp.U == 30) ||
+      kp.B > 15 || kp.tab_m <= 0 || cells >= 65536 || c->d2max < 0)
+    return MEV_OK;
+  const int NB = kp.nb_cls, NU = kp.nu_cls;
+  const size_t r100_off = up16(2 * cells), st_off = r100_off + 8 * 72;
+  const size_t rate_off = up16(st_off + 8 * (size_t)NU * kp.B);
+  const size_t one_wave = lds2_per_wave(kp.envs_per_wave, kp.B, kp.tab_m, 1) +
+                          (size_t)2 * kp.envs_per_wave * kStage2Bytes + 4;
+  if (rate_off + one_wave + 8 * 64 > (size_t)kLds2BytesPerWG) return MEV_OK;
+  const int cap = (int)(((size_t)kLds2BytesPerWG - rate_off) / 8);
+  c->het_reach = c->d2max;
+  c->het_nwords = c->d2max / 32 + 1;
+  const size_t nd = (size_t)c->d2max + 1;
+  if (hipMalloc(&c->het_cell, sizeof(int2) * cells) != hipSuccess ||
+      hipMalloc(&c->het_flag, (size_t)NB * nd) != hipSuccess ||
+      hipMalloc(&c->het_words, sizeof(uint2) * (size_t)NB * (c->het_nwords + 1)) != hipSuccess ||
+      hipMalloc(&c->het_info, sizeof(int) * (2 + 2 * (size_t)NB * NU)) != hipSuccess ||
+      hipMalloc(&c->het_blob, rate_off + 8 * (size_t)cap) != hipSuccess)
+    return MEV_ENOMEM;
+  MEV_HIP(hipMemset(c->het_blob, 0, rate_off + 8 * (size_t)cap));
+  MEV_HIP(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(c->het_blob), 0xF000, cells));
+  double r100[72] = {0.0};
+  for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
+  MEV_HIP(hipMemcpy(c->het_blob + r100_off, r100, sizeof(r100), hipMemcpyHostToDevice));
+  const int zero = 0;
+  MEV_HIP(hipMemcpy(c->het_info, &zero, sizeof(int), hipMemcpyHostToDevice));
+  c->het_r100_off = (int)r100_off;
+  c->het_st_off = (int)st_off;
+  c->het_rate_off = (int)rate_off;
+  c->het_rate_cap = cap;
+  MEV_HIP(hipDeviceGetAttribute(&c->het_cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  c->het_lds = 1;
+  return MEV_OK;
+}
+
 static KTables tables_of(const mev_ctx* c) {
   KTables tb{};
   tb.rate_full = c->rate_full;
@@ -4387,6 +4715,18 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     if (std::isfinite(kmax) && kmax < (double)(1 << 22)) {
       kp.util_direct = 0;
       kp.util_kmax = (int)kmax;
+      // the float32 utility's absolute error (utility_f32r), twice the sum of: the rate's float32
+      // rounding and w2's (3 ulp relative, 2.2e-8 for 0.01f) through log2 (1 / ln 2 per relative
+      // unit) times the slope A = |w1 ln2 / ln w3 * scale|; v_log_f32 (taken as 2 ulp of
+      // max(|log2 x|, 1) over the table's rates, x = w2 + 0.01 .. w2 + r_sat); the products,
+      // clip bounds and offset (2 ulp each of max(|lower|, |upper|) * scale, 1, |offset|)
+      const double A = fabs(kp.w1 * log(2.0) / kp.log_w3 * (2.0 / (kp.upper - kp.lower)));
+      const double lmax = std::max({1.0, fabs(log2(kp.w2 + 0.01)), fabs(log2(kp.w2 + std::max(r_sat, 0.01)))});
+      const double off = fabs(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
+      const double sc = std::max(fabs(kp.lower), fabs(kp.upper)) * 2.0 / (kp.upper - kp.lower);
+      kp.u_err = (float)(2.0 * (A * ((3.0 * 0x1p-24 + 2.2e-8) / log(2.0) + 0x1p-22 * lmax) +
+                               0x1p-22 * (1.0 + off + sc)));
+      if (params->reward_exact > 0) kp.u_err = INFINITY;  // (every row takes the exact path)
     }
   }
 
@@ -4487,7 +4827,12 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
       return rc;
     }
   }
-  if (c->blob && c->kp.lds_mode == 3) {  // |D| of each layout, read back without a stream sync
+  if (c->het_packed) {
+    rc = build_het_lds(c);
+    if (rc) return rc;
+  }
+  if ((c->blob && c->kp.lds_mode == 3) || c->het_lds) {  // |D| (mode 3) / the rate count (mode 5)
+                                                       // of each layout, read back without a sync
     MEV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->dcount_pin), sizeof(int), hipHostMallocDefault));
     MEV_HIP(hipEventCreateWithFlags(&c->ev_dcount, hipEventDisableTiming));
   }
@@ -4565,7 +4910,8 @@ void mev_destroy(mev_ctx* c) {
   if (c->tab_st) (void)hipFree(c->tab_st);
   if (c->drawn) (void)hipFree(c->drawn);
   for (void* h : {(void*)c->h_bcl, (void*)c->h_ucl, (void*)c->h_pair, (void*)c->h_mv,
-                  (void*)c->h_perm, (void*)c->h_seg})
+                  (void*)c->h_perm, (void*)c->h_seg, (void*)c->het_cell, (void*)c->het_flag,
+                  (void*)c->het_words, (void*)c->het_info, (void*)c->het_blob})
     if (h) (void)hipFree(h);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -4761,6 +5107,64 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       MEV_HIP(hipGetLastError());
       c->last_kind = MEV_KIND_LDS2_PERENV;
       return MEV_OK;
+    }
+    // heterogeneous entities with a shared layout: k_steps_lds2 HET on the lds_mode 5 tables
+    // (build_het_lds) when the layout's rates fit beside at least one wavefront
+    if (c->het_lds && lean && traj && pre_ok && c->p.two_groups >= 0 && c->p.two_groups <= 2) {
+      const int nrate = layout_dcount(c);
+      if (nrate >= 0 && nrate <= c->het_rate_cap) {
+        // one group per wavefront unless two_groups = 1: at 65,536 mobile-large-mixed envs 2.95 vs
+        // 4.04 ms per 200-step launch (the tables leave room for ~10 two-group waves per
+        // workgroup, 2.5 per SIMD, against 16 one-group waves)
+        const int R = c->p.two_groups == 1 ? 2 : 1;
+        const int G = kp.envs_per_wave;
+        const int units = R == 2 ? pairs : groups;
+        const size_t blob = ((size_t)c->het_rate_off + 8 * (size_t)nrate + 15) & ~(size_t)15;
+        const int srows = std::max(1, std::min(c->stage_cap > 0 ? c->stage_cap : kLds2Window, nsteps));
+        const bool dbl = 2 * nsteps > srows;
+        const size_t row_w = (size_t)G * R * kStage2Bytes;  // a staged row, per wave
+        const size_t per_w = lds2_per_wave(G, kp.B, kp.tab_m, R) + (size_t)(dbl ? 2 : 1) * srows * row_w;
+        const int fit = blob + 4 + per_w <= (size_t)kLds2BytesPerWG
+                            ? (int)(((size_t)kLds2BytesPerWG - blob - 4) / per_w) : 0;
+        if (fit >= 1) {
+          const bool c8 = kp.st8 != 0;
+          StepsKernel k2 =
+              kp.U == 15 ? (R == 2 ? (c8 ? k_steps_lds2<15, 0, false, false, 2, true, false, true>
+                                         : k_steps_lds2<15, 0, false, false, 2, false, false, true>)
+                                   : (c8 ? k_steps_lds2<15, 0, false, false, 1, true, false, true>
+                                         : k_steps_lds2<15, 0, false, false, 1, false, false, true>))
+                         : (R == 2 ? (c8 ? k_steps_lds2<30, 0, false, false, 2, true, false, true>
+                                         : k_steps_lds2<30, 0, false, false, 2, false, false, true>)
+                                   : (c8 ? k_steps_lds2<30, 0, false, false, 1, true, false, true>
+                                         : k_steps_lds2<30, 0, false, false, 1, false, false, true>));
+          const int nw2 = std::max(1, std::min({kLds2Waves, fit, (units + c->het_cus - 1) / c->het_cus}));
+          const size_t sh = blob + nw2 * lds2_per_wave(G, kp.B, kp.tab_m, R) +
+                            (((size_t)(dbl ? 2 : 1) * srows * nw2 * row_w + 3) & ~(size_t)3);
+          const size_t key = (sh << 8) | ((size_t)nw2 << 2) | ((size_t)R << 1) | (c8 ? 1u : 0u);
+          if (c->het_occ_key != key) {
+            int n = 0;
+            MEV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &n, reinterpret_cast<const void*>(k2), 64 * nw2, sh));
+            c->het_occ_key = key;
+            c->het_occ_n = std::max(1, n);
+          }
+          const int blocks = std::min((units + nw2 - 1) / nw2, c->het_cus * c->het_occ_n);
+          KParams kp5 = kp;
+          kp5.lds_mode = 5;
+          kp5.lds_assoc = (int)blob;
+          kp5.lds_st_off = c->het_st_off;
+          kp5.lds_rate_off = c->het_rate_off;
+          kp5.lds_r100_off = c->het_r100_off;
+          KTables tb5 = tb;
+          tb5.lds_blob = reinterpret_cast<const int4*>(c->het_blob);
+          tb5.dcount = nullptr;
+          launch_k(k2, dim3(blocks), dim3(64 * nw2), sh, stream, ev, kp5, ks, ko, tb5, groups,
+                   nsteps, 1, dbl ? -srows : srows);
+          MEV_HIP(hipGetLastError());
+          c->last_kind = MEV_KIND_LDS2_HET;
+          return MEV_OK;
+        }
+      }
     }
     // two groups per wavefront once the pairs fill every resident workgroup, else the
     // one-group packed kernel below. mev_params.two_groups (A/B switches): -1 the packed kernel
@@ -5005,6 +5409,29 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
                        c->p.height, c->h_bcl, c->h_pair, c->kp.nu_cls, c->rate_full, c->assoc);
     MEV_HIP(hipGetLastError());
+    if (c->het_lds) {  // the two-group rollout's tables (lds_mode 5), see build_het_lds
+      const int NB = c->kp.nb_cls, NU = c->kp.nu_cls, reach = c->het_reach, nw = c->het_nwords;
+      const int nd = reach + 1;
+      hipStream_t s = (hipStream_t)stream;
+      MEV_HIP(hipMemsetAsync(c->het_flag, 0, (size_t)NB * nd, s));
+      hipLaunchKernelGGL(k_het_cells, dim3((cells + 255) / 256), dim3(256), 0, s,
+                         reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
+                         c->p.height, reach, c->h_bcl, c->het_cell, c->het_flag);
+      for (int cb = 0; cb < NB; ++cb)
+        hipLaunchKernelGGL(k_d2_prefix, dim3(1), dim3(1024), 0, s, c->het_flag + (size_t)cb * nd,
+                           nd, c->het_words + (size_t)cb * (nw + 1), nw);
+      hipLaunchKernelGGL(k_het_info, dim3(1), dim3(64), 0, s, c->het_words, nw, NB, NU,
+                         c->p.num_bs, c->h_bcl, c->h_pair, reach,
+                         reinterpret_cast<int2*>(c->het_blob + c->het_st_off), c->het_info);
+      const int n = std::max(cells, NB * nd);
+      hipLaunchKernelGGL(k_het_map, dim3((n + 255) / 256), dim3(256), 0, s, c->het_cell, cells,
+                         c->het_words, nw, reach, NB, NU, c->h_bcl, c->h_pair, c->rate_full,
+                         c->het_info, c->het_blob, c->het_rate_off, c->het_rate_cap);
+      MEV_HIP(hipGetLastError());
+      MEV_HIP(hipMemcpyAsync(c->dcount_pin, c->het_info, sizeof(int), hipMemcpyDeviceToHost, s));
+      MEV_HIP(hipEventRecord(c->ev_dcount, s));
+      c->dcount_pending = 1;
+    }
     return MEV_OK;
   }
   hipLaunchKernelGGL(k_assoc_map, dim3((cells + 255) / 256), dim3(256), 0, (hipStream_t)stream,

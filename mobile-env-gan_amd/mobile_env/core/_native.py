@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -55,6 +55,7 @@ class MevParams(C.Structure):
         ("ues_per_lane", C.c_int32),
         ("ue_velocity", C.c_void_p),
         ("compact_state", C.c_int32),
+        ("reward_exact", C.c_int32),
     ]
 
 

@@ -78,6 +78,9 @@ class EngineParams:
     # UE state form (mev_params.compact_state): 0 auto -- uint8 x4 per UE on maps <= 255 per
     # side (every registered scenario), else int16 x4; -1 always int16; 1 uint8 (maps <= 255)
     compact_state: int = 0
+    # mev_params.reward_exact: 1 -- every float32 reward from the exact float64 utilities (the
+    # lean kernels otherwise do that only where the float32 sum could miss 1e-5 relative)
+    reward_exact: int = 0
 
     @property
     def state_u8(self) -> bool:
@@ -162,7 +165,7 @@ class EngineParams:
             stage_rows=int(self.stage_rows), xcd_remap=int(self.xcd_remap),
             scenario_constants=int(self.scenario_constants),
             station_culling=int(self.station_culling), ues_per_lane=int(self.ues_per_lane),
-            compact_state=int(self.state_u8),
+            compact_state=int(self.state_u8), reward_exact=int(self.reward_exact),
             ue_velocity=(arr([float(v) for v in self.ue_velocity], np.float64)
                          if self.ue_velocity is not None else C.c_void_p(None)))
         cp._keep = keep
@@ -363,7 +366,7 @@ class StepEngine:
     #: mev_last_launch_kind codes (include/mev.h MEV_KIND_*)
     LAUNCH_KINDS = {0: None, 1: "packed_step", 2: "packed_fused", 3: "lds2_two_groups",
                     4: "lds2_one_group", 5: "lds2_pipelined", 6: "lds2_per_env", 7: "block",
-                    8: "lds2_pipelined_seg32"}
+                    8: "lds2_pipelined_seg32", 9: "lds2_het"}
 
     @property
     def last_launch_kind(self) -> "str | None":

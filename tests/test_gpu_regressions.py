@@ -118,3 +118,59 @@ def test_layout_change_then_pipelined_rollout_vs_oracle():
     ob = OracleBatch(OracleParams(), new_bs.tolist(), U, seeds)
     assert_rollout_vs_oracle(tr, ob, 45)
     eng.close()
+
+
+def _exact_case(case):
+    """(engine params, layout, oracle params, expected launch kind) of a reward_exact case."""
+    from mobile_env.core.engine import EngineParams
+    from mobile_env.scenarios.registry import LAYOUTS, spec
+    from oracle.vec import OracleParams
+    if case == "mixed":
+        c = spec("mobile-large-mixed-v0")["classes"]
+        L = LAYOUTS["large"]
+        kw = dict(bs_classes=c["bs_classes"], ue_classes=c["ue_classes"], bs_class=c["bs_class"],
+                  ue_class=c["ue_class"])
+        return (dict(num_ues=L["num_ues"], num_bs=len(L["bs"]), **kw), L["bs"], OracleParams(**kw),
+                2000, "lds2_het")
+    if case == "block":
+        rng = np.random.default_rng(3)
+        bs = rng.integers(0, 200, size=(40, 2)).astype(np.int32)
+        return dict(num_ues=100, num_bs=40, velocity=4.0), bs, OracleParams(velocity=4.0), 64, "block"
+    size, vel, E, kind = {"two": ("large", 1.5, 16500, "lds2_two_groups"),
+                          "pipe30": ("large", 1.5, 512, "lds2_pipelined"),
+                          "pipe15": ("medium", 1.5, 512, "lds2_pipelined"),
+                          "packed": ("small", 1.5, 512, "packed_fused"),
+                          "generic": ("large", 10.0, 512, "packed_fused")}[case]
+    L = LAYOUTS[size]
+    return (dict(num_ues=L["num_ues"], num_bs=len(L["bs"]), velocity=vel), L["bs"],
+            OracleParams(velocity=vel), E, kind)
+
+
+@pytest.mark.parametrize("case", ["two", "pipe30", "pipe15", "packed", "generic", "mixed", "block"])
+def test_reward_exact_every_kernel_vs_oracle(case):
+    """reward_exact = 1 sends every env-step's reward through the exact path that the lean
+    kernels otherwise take only where the float32 sum could miss 1e-5 relative (reward_risky:
+    mean utilities near zero) -- the two-group step's in-step path, the pipelined loop's flush,
+    the packed kernels' leaders, the block kernel's row finish, the heterogeneous tables: 25
+    rollout steps (a reset inside) and 3 one-step launches, the rewards within one float32 ulp
+    of the oracle's float64 mean (atol 0), every other output as the oracle's."""
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from oracle.vec import OracleBatch
+    kw, bs, op, E, kind = _exact_case(case)
+    seeds = 4242 + 13 * np.arange(E)
+    eng = StepEngine(EngineParams(num_envs=E, reward_exact=1, **kw), bs, seeds, device="cuda")
+    n = 25
+    tr = eng.rollout(n)
+    assert eng.last_launch_kind == kind
+    ob = OracleBatch(op, bs, kw["num_ues"], seeds)
+    for s in range(n):
+        o = ob.step()
+        np.testing.assert_array_equal(tr.serving[s].cpu().numpy(), o["serving"], err_msg=f"step {s}")
+        np.testing.assert_allclose(tr.reward[s].cpu().numpy(), o["metrics"][:, 2].astype(np.float32),
+                                   rtol=1.2e-7, atol=0, err_msg=f"reward step {s}")
+    for s in range(3):
+        eng.step()
+        o = ob.step()
+        np.testing.assert_allclose(eng.reward.cpu().numpy(), o["metrics"][:, 2].astype(np.float32),
+                                   rtol=1.2e-7, atol=0, err_msg=f"one-step reward {s}")
+    eng.close()

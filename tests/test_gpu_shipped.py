@@ -14,7 +14,9 @@ every step's outputs with the oracle (oracle/vec.py, pinned to the reference's f
 * BASELINE configs[2] (the bench): mobile-large-central-v0 at 65,536 envs -> the two-group
   scenario kernel; every 16th env (4,096 of them) against the oracle run on those envs' seeds
   -- envs are independent, so the subset comparison is exact;
-* the Gym step() launch of both (mev_step(1), one launch per step).
+* the Gym step() launch of both (mev_step(1), one launch per step);
+* the build-defined mobile-large-mixed-v0 (heterogeneous classes) at 65,536 envs -> the
+  two-group kernel on the lds_mode 5 tables, every 16th env against the oracle.
 
 Bars (north_star): positions, serving, done bit-exact; float32 rate / utility / reward within
 1e-5 relative (rewards of magnitude >= 1e-3 with atol 0, helpers.assert_step_vs_oracle).
@@ -99,3 +101,31 @@ def test_gym_step_shipped_vs_oracle(env_id, size, E, stride):
                               trunc.index_select(0, ti).cpu().numpy(), where=f"step {s}")
         assert not bool(term.any())
     env.close()
+
+
+def test_mixed_65536_rollout_strided_vs_oracle():
+    """mobile-large-mixed-v0 at the bench's batch (three station and three UE classes on the
+    large layout; entities.py:7-45): the heterogeneous two-group LDS kernel, one 45-step rollout,
+    every 16th env against the oracle with the same classes."""
+    import mobile_env
+    import torch
+    from mobile_env.scenarios.registry import LAYOUTS, spec
+    from oracle.vec import OracleBatch, OracleParams
+    E, n, stride = 65536, 45, 16
+    env = mobile_env.make("mobile-large-mixed-v0", num_envs=E, device="cuda:0", seed=3000)
+    env.reset()
+    eng = env.engine
+    tr = eng.rollout(n)
+    assert eng.last_launch_kind == "lds2_het"
+    c = spec("mobile-large-mixed-v0")["classes"]
+    idx = np.arange(0, E, stride)
+    L = LAYOUTS["large"]
+    ob = OracleBatch(OracleParams(bs_classes=c["bs_classes"], ue_classes=c["ue_classes"],
+                                  bs_class=c["bs_class"], ue_class=c["ue_class"]),
+                     L["bs"], L["num_ues"], env.seeds.numpy()[idx])
+    o = assert_rollout_vs_oracle(tr, ob, n, env_idx=idx)
+    ti = torch.as_tensor(idx, device=eng.device)
+    np.testing.assert_array_equal(eng.ue_xy.index_select(0, ti).cpu().numpy(), o["xy"])
+    del tr
+    env.close()
+    torch.cuda.empty_cache()
