@@ -381,6 +381,42 @@ __device__ __forceinline__ void move_ue_p(int2& pos, int2& wp, const MoveP& mp) 
   }
 }
 
+// move_ue_p with the parameters held compactly (the heterogeneous two-group rollout keeps them
+// per lane for the launch): {vel_f, move_lim} and hpk = d2snap << 8 | axis_exact << 4 | class;
+// the float64 velocity of the exact paths (axis moves, ties) read from `mvu` there (rare).
+__device__ __forceinline__ void move_ue_pc(int2& pos, int2& wp, float vel_f, float move_lim,
+                                           uint32_t hpk, const MoveP* mvu) {
+  const int dx = wp.x - pos.x;
+  const int dy = wp.y - pos.y;
+  const int d2 = __mul24(dx, dx) + __mul24(dy, dy);
+  if (d2 <= (int)(hpk >> 8)) {
+    pos = wp;
+    wp = make_int2(-1, -1);
+    return;
+  }
+  const uint32_t axis = (hpk >> 4) & 3u;
+  if (axis == 2u) {
+    pos = step_v15(pos, dx, dy, __mul24(dx, dx), __mul24(dy, dy));
+    return;
+  }
+  if (axis && (dx == 0 || dy == 0)) {
+    const double q = mvu->vel;
+    if (dy == 0) pos.x = (int)rint((double)pos.x + (dx > 0 ? q : -q));
+    else pos.y = (int)rint((double)pos.y + (dy > 0 ? q : -q));
+    return;
+  }
+  const float sc = vel_f * __builtin_amdgcn_rsqf((float)d2);
+  const float qx = (float)dx * sc;
+  const float qy = (float)dy * sc;
+  const float rx = rintf(qx), ry = rintf(qy);
+  if (fmaxf(fabsf(qx - rx), fabsf(qy - ry)) < move_lim) {
+    pos.x += (int)rx;
+    pos.y += (int)ry;
+  } else {
+    pos = move_exact(pos, dx, dy, mvu->vel);
+  }
+}
+
 // The context's movement parameters (compile-time constants in a scenario instance).
 template <int SCN>
 constexpr bool scn_v15() { return SCN != 0 && scn_const(SCN).vel_f == 0x3fc00000u; }
@@ -570,9 +606,44 @@ __device__ __forceinline__ long long util_fix50(double cents, bool take, const K
   const double uu = cents <= (double)kp.util_kmax ? tab[(int)cents] : kp.util_sat;
   return (long long)(uu * 0x1p50);
 }
+// The guard's constants held in LDS where a kernel's scalar registers are scarce (read only by
+// the rare path and the flush's test): {utility table, util_sat, util_kmax, u_err} as four
+// 8-byte slots -- the r100 table's slots 66..69 of the LDS blobs (kRewardCSlot), or a static
+// array of the block kernel. Loop-invariant kernel arguments used there were kept in SGPRs
+// across the step loops and spilled others to VGPR lanes (+9 % at 4,096 medium envs).
+constexpr int kRewardCSlot = 66;
+struct RewardC {
+  const double* tab;
+  double sat;
+  double kmax;
+  float u_err;
+};
+__device__ __forceinline__ RewardC reward_c(const char* p) {  // (p: 8-byte aligned LDS)
+  RewardC c;
+  c.tab = *reinterpret_cast<const double* const*>(p);
+  c.sat = *reinterpret_cast<const double*>(p + 8);
+  c.kmax = *reinterpret_cast<const double*>(p + 16);
+  c.u_err = *reinterpret_cast<const float*>(p + 24);
+  return c;
+}
+__device__ __forceinline__ long long util_fix50c(double cents, const RewardC& c) {
+  const double uu = cents <= c.kmax ? c.tab[(int)cents] : c.sat;
+  return (long long)(uu * 0x1p50);
+}
+__device__ __forceinline__ bool reward_risky_c(float sum, int nact, float q, float u_err) {
+  return nact > 0 && fabsf(sum) * 9.5e-6f <= (float)nact * (u_err + q);
+}
 __device__ __forceinline__ float exact_mean50(long long s, int nact) {
   return (float)((double)s * 0x1p-50 / (double)nact);
 }
+// The guard's rare work out of line under MEV_GUARD_CALL: one copy of the code, whose scalars
+// then do not compete with the step loops' (inlined into a loop, they kept kernel arguments
+// live across it and spilled others to VGPR lanes).
+#ifdef MEV_GUARD_CALL
+#define MEV_GUARD_FN __device__ __attribute__((noinline))
+#else
+#define MEV_GUARD_FN __device__ __forceinline__
+#endif
 template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ long long dpp_i64(long long v) {
   const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(unsigned long long)v, CTRL, ROWMASK, 0xf, true);
@@ -861,6 +932,16 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 //         `lblob` (KTables::lds_blob) instead of the L2 gather: 1 = station map + rank index
 //         (four dependent reads), 2 = station map + per-cell rank map (two parallel reads and
 //         the rate).
+// packed_group's rare exact mean (wave-wide; valid in the env's leader lane): cents < 0 for a
+// lane that does not count
+template <bool ROWS, int PC>
+MEV_GUARD_FN float packed_fix(double cents, int U, int u, const double* tab, double kmax,
+                              double sat, int nact) {
+  const long long v = cents < 0.0 ? 0 : util_fix50c(cents, RewardC{tab, sat, kmax, 0.f});
+  const long long se = ROWS ? seg_lsum_rows<PC>(v) : seg_lsum(v, U, u);
+  return exact_mean50(se, nact);
+}
+
 template <bool PER_ENV_BS, bool LEAN, int UC, bool FUSED, int LDSM = 0, int SCN = 0,
           bool STG = false, bool TF = false>
 __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st,
@@ -1241,14 +1322,18 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   bool use_exact = false;
   float exact_r = 0.f;
   if constexpr (LEAN) {
+    // (the constants from the LDS blob's RewardC where there is one)
+    const char* rcp = LDSA ? lblob + KPS(lds_r100_off) + 8 * kRewardCSlot : nullptr;
+    const float u_err = LDSA ? *reinterpret_cast<const float*>(rcp + 24) : kp.u_err;
     const bool risky = env_ok && leader &&
-                       reward_risky(ISUM ? (float)isum_u * 0x1p-25f : (float)sum_u, nact,
-                                    ISUM ? 0x1p-25f : 0.f, kp);
+                       reward_risky_c(ISUM ? (float)isum_u * 0x1p-25f : (float)sum_u, nact,
+                                      ISUM ? 0x1p-25f : 0.f, u_err);
     if (bal(risky)) {
-      const long long v = util_fix50(cents, active, kp, tb.util);
-      const long long se = ROWS ? seg_lsum_rows<PC>(v) : seg_lsum(v, U, u);
+      const RewardC c = LDSA ? reward_c(rcp)
+                             : RewardC{tb.util, kp.util_sat, (double)kp.util_kmax, kp.u_err};
+      const float ex = packed_fix<ROWS, PC>(active ? cents : -1.0, U, u, c.tab, c.kmax, c.sat, nact);
       use_exact = risky;
-      exact_r = exact_mean50(se, nact);
+      exact_r = ex;
     }
   }
   double sum_r = 0.0;
@@ -1647,6 +1732,13 @@ __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
 // drawn = M + 1. Measured: the flag-free form 101 vs 104 us per 200-step launch at 4,096 medium
 // envs, but 1.55 vs 1.51 ms at 65,536 large envs in the two-group loop, interleaved on one box.)
 constexpr int kSok = 1, kMov = 2;
+// Heterogeneous LDS tables: lds_mode 6 (a 4-bit station map, station coordinates | class, the
+// classes' rank indices -- half the bytes of mode 5's u16 cell entries) unless MEV_HET_U16
+#ifdef MEV_HET_U16
+constexpr bool kHetNib = false;
+#else
+constexpr bool kHetNib = true;
+#endif
 struct Ctx2 {
   int t, drawn, fl;
   int2 pos, wp;
@@ -1667,7 +1759,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                                           const char* __restrict__ lblob, u128* __restrict__ lpcg,
                                           int* __restrict__ hist, const int* __restrict__ ltab,
                                           int* __restrict__ srow, const int* __restrict__ lkeys,
-                                          int hcu = 0, const MoveP& hmv = MoveP{}) {
+                                          uint32_t hpk = 0, float hvf = 0.f, float hml = 0.f) {
   constexpr int PC = pitch_of(UC), U = ue_of(UC), G = 64 / PC;
   const int M = KPS(tab_m), B = KPS(B), HS = lds2_hist_stride(G, B);
   const int u = m.u;
@@ -1796,7 +1888,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       int2 p = c[r].pos, w = c[r].wp;
-      if (active[r]) move_ue_p(p, w, hmv);
+      if (active[r]) move_ue_pc(p, w, hvf, hml, hpk, tb.mv + min(m.u, U - 1));
       c[r].pos = p;
       c[r].wp = w;
     }
@@ -1877,6 +1969,46 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
       cell[r] = ent[r] = 0;
     }
+  } else if (HET && kHetNib) {
+    // mode 6: s* per cell (4 bits, 15: none within reach), its coordinates and class, d2 to it,
+    // the rank k of d2 in D of its class (the class's rank index); per (UE class, station) the
+    // pair's {rate offset, largest connectable rank} (read beside the coordinates)
+    const int cells = KPS(W) * KPS(H);
+    const uint32_t nwd = (uint32_t)kp.d2max / 32u + 1u, reach = (uint32_t)kp.d2max;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
+                    (uint32_t)(cells - 1));
+      const uint32_t nib =
+          ((uint32_t)*reinterpret_cast<const uint8_t*>(lblob + (cell[r] >> 1)) >> ((cell[r] & 1u) << 2)) & 15u;
+      const bool has = nib != 15u;
+      const uint32_t s = has ? nib : 0u;
+      const uint32_t sp = *reinterpret_cast<const uint32_t*>(lblob + kp.lds_st_off + 4u * s);
+      const int2 pk = *reinterpret_cast<const int2*>(lblob + kp.lds_r16_off +
+                                                     8u * ((hpk & 15u) * (uint32_t)B + s));
+      const int dx = c[r].pos.x - (int)(sp & 4095u), dy = c[r].pos.y - (int)((sp >> 12) & 4095u);
+      const uint32_t d2 = (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
+      const uint32_t dq = min(d2, reach);
+      const uint2 w = *reinterpret_cast<const uint2*>(lblob + kp.lds_rank_off +
+                                                      8u * ((sp >> 24) * (nwd + 1u) + (dq >> 5)));
+      const uint32_t k = w.y + (uint32_t)__popc(w.x & ((1u << (dq & 31u)) - 1u));
+      const bool conn = has && d2 <= reach && (int)k <= pk.y && k < 4095u;  // (runs: <= 4,095, k_het_info)
+      full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) +
+                                                 8u * (conn ? (uint32_t)pk.x + k : 0u));
+      srv[r] = active[r] && conn ? (int)s : -1;
+      // s* out of this class's reach (another station may serve it): the class's L2 map
+      const bool fb = active[r] && has && !conn;
+      if (bal(fb) & act_w[r]) {
+        if (fb) {
+          const int4 q = at(const_cast<int4*>(tb.assoc),
+                            16u * ((hpk & 15u) * (uint32_t)cells + cell[r]));
+          srv[r] = q.x;
+          full[r] = __hiloint2double(q.w, q.z);
+        }
+        wait_vmem();
+      }
+      ent[r] = 0;
+    }
   } else if (HET) {
     // {s*, rank k of d2 in D of s*'s class} per cell; per (UE class, station): {the offset of
     // the pair's rates over that D, the pair's largest connectable rank}
@@ -1889,7 +2021,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       const bool has = ent[r] < 0xF000u;
       const uint32_t s = has ? ent[r] >> 12 : 0u, k = has ? ent[r] & 4095u : 0u;
       const int2 pk = *reinterpret_cast<const int2*>(lblob + kp.lds_st_off +
-                                                     8u * ((uint32_t)hcu * (uint32_t)B + s));
+                                                     8u * ((hpk & 15u) * (uint32_t)B + s));
       const bool conn = has && (int)k <= pk.y;
       full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) +
                                                  8u * (conn ? (uint32_t)pk.x + k : 0u));
@@ -1900,7 +2032,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       if (bal(fb) & act_w[r]) {
         if (fb) {
           const int4 q = at(const_cast<int4*>(tb.assoc),
-                            16u * ((uint32_t)hcu * (uint32_t)cells + cell[r]));
+                            16u * ((hpk & 15u) * (uint32_t)cells + cell[r]));
           srv[r] = q.x;
           full[r] = __hiloint2double(q.w, q.z);
         }
@@ -2290,6 +2422,27 @@ __device__ __forceinline__ void lds_barrier() {
 // `trailing`: a second barrier after the reads, before the window's slots are written again
 // (not needed when consecutive pairs alternate between two windows: the next write of this
 // window follows the next flush's first barrier, which every reader here has passed).
+// The flush's rare fix-up (see flush_staged2).
+MEV_GUARD_FN void flush_fix(const int* srow, const float* obs_f, float* rew, const char* rc, int E,
+                            int e0, int row0, int nr, int NWG, int U) {
+  const float inv_nwg = 1.0f / (float)NWG;
+  const RewardC c = reward_c(rc);
+#pragma unroll 1
+  for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
+    const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
+    if (e0 + j >= E) continue;
+    const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
+    const uint32_t b = (uint32_t)v.y;
+    const int nact = (int)(b & 0x7fu);
+    if ((b & 0x100u) || !reward_risky_c((float)v.x * 0x1p-25f, nact, 0x1p-25f, c.u_err)) continue;
+    const float* rates = obs_f + 4 * ((size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)) * (size_t)U + 2;
+    long long su = 0;
+#pragma unroll 1
+    for (int u = 0; u < U; ++u) su += util_fix50c(rint((double)rates[4 * u] * 100.0), c);
+    rew[(size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)] = exact_mean50(su, nact);
+  }
+}
+
 // DETECT (the pipelined loop, whose steps do not test reward_risky): the flush tests every row's
 // fixed-point sum, and if any row of the workgroup's window is risky (block-uniform, one
 // __syncthreads_or per flush) re-forms those rows' rewards from the exact utilities of the
@@ -2299,11 +2452,12 @@ __device__ __forceinline__ void lds_barrier() {
 template <bool DETECT = false>
 __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, int E, int e0,
                                               int row0, int nr, float lower, int NWG,
-                                              bool trailing = true, const KParams* kp = nullptr,
-                                              const double* utab = nullptr, int U = 0) {
+                                              bool trailing = true, const char* rc = nullptr,
+                                              int U = 0) {
   lds_barrier();
   const float inv_nwg = 1.0f / (float)NWG;
   bool any = false;
+  const float u_err = DETECT ? *reinterpret_cast<const float*>(rc + 24) : 0.f;
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     // q / NWG through float (q + 1/2 is >= 1/2 away from a multiple of NWG; exact for q < 2^22)
     const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
@@ -2318,30 +2472,15 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
           (b & 0x100u) ? __int_as_float(v.x)
                        : nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
       at(out.done + ro, o) = (uint8_t)((b >> 7) & 1u);
-      if (DETECT) any = any || (!(b & 0x100u) && reward_risky((float)v.x * 0x1p-25f, nact, 0x1p-25f, *kp));
+      if (DETECT) any = any || (!(b & 0x100u) && reward_risky_c((float)v.x * 0x1p-25f, nact, 0x1p-25f, u_err));
     }
   }
   if (DETECT && __syncthreads_or(any)) {  // rare
     __syncthreads();  // (fenced: the window's obs stores of every wave visible)
-    // (rolled loops, the pointers laundered inside the branch: inlined into the step loop, an
-    // unrolled fix-up held ~20 VGPRs across it)
     const float* obs_f = reinterpret_cast<const float*>(out.obs);
     float* rew = out.reward;
-    asm volatile("" : "+s"(obs_f), "+s"(rew), "+s"(utab));
-#pragma unroll 1
-    for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
-      const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
-      if (e0 + j >= E) continue;
-      const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
-      const uint32_t b = (uint32_t)v.y;
-      const int nact = (int)(b & 0x7fu);
-      if ((b & 0x100u) || !reward_risky((float)v.x * 0x1p-25f, nact, 0x1p-25f, *kp)) continue;
-      const float* rates = obs_f + 4 * ((size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)) * (size_t)U + 2;
-      long long su = 0;
-#pragma unroll 1
-      for (int u = 0; u < U; ++u) su += util_fix50(rint((double)rates[4 * u] * 100.0), true, *kp, utab);
-      rew[(size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)] = exact_mean50(su, nact);
-    }
+    asm volatile("" : "+s"(obs_f), "+s"(rew));
+    flush_fix(srow, obs_f, rew, rc, E, e0, row0, nr, NWG, U);
   }
   if (trailing) lds_barrier();
 }
@@ -2593,8 +2732,15 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
   const int pb0 = block_slot(kp.xcd_remap) * NW;
   static_assert(!HET || (SCN == 0 && !PE && !PIPE), "HET: the generic shared-layout instance");
   // (HET) this lane's UE class and movement parameters, for the launch
-  const int hcu = HET ? (int)tb.ue_cls[min(m.u, U - 1)] : 0;
-  const MoveP hmv = HET ? tb.mv[min(m.u, U - 1)] : MoveP{};
+  // (the class and movement parameters packed: three registers, move_ue_pc)
+  uint32_t hpk = 0;
+  float hvf = 0.f, hml = 0.f;
+  if (HET) {
+    const MoveP mv = tb.mv[min(m.u, U - 1)];
+    hpk = ((uint32_t)mv.d2snap << 8) | ((uint32_t)mv.axis_exact << 4) | (uint32_t)tb.ue_cls[min(m.u, U - 1)];
+    hvf = mv.vel_f;
+    hml = mv.move_lim;
+  }
   constexpr int NT = lds2_pre_words<UC, SCN, R>();
   constexpr int NK = PE ? (R * G * 16 + 63) / 64 : 1;
   Pre2<R, NT, NK> f;  // the inputs of the wave's next pair
@@ -2667,7 +2813,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           int* const win = sw + (dbl ? 2 * hcur * wrows : 0);
           lds2_step<UC, SCN, R, PE, TF, decltype(full)::value, HET>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
-              win + 2 * (sr * NWG + wvu * G * R), lkeys, hcu, hmv);
+              win + 2 * (sr * NWG + wvu * G * R), lkeys, hpk, hvf, hml);
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps)) {
             flush_staged2(out, win, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, !dbl);
             if (dbl) hcur ^= 1;
@@ -2698,8 +2844,8 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
           pipe_emit_back<UC, SCN, TF>(kp, out, m, q, ef, e[0], nok[0], klead, traj ? i : 0,
                                       hist, sw + 2 * (sr * NWG + wvu * G));
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps))
-            flush_staged2<true>(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true, &kp,
-                                tb.util, U);
+            flush_staged2<true>(out, sw, kp.E, e0, traj ? i - sr : 0, sr + 1, lower, NWG, true,
+                                lblob + KPS(lds_r100_off) + 8 * kRewardCSlot, U);
           ++i;
           sr = sr + 1 == stage_rows ? 0 : sr + 1;
         };
@@ -2766,12 +2912,14 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
       MEV_TS(min(4 + 3 * it, 28));
     }
     if (alt) {
-      flush_staged2<PIPE>(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false, &kp, tb.util, U);
+      flush_staged2<PIPE>(out, sw, kp.E, e0, 0, nsteps, lower, NWG, false,
+                          lblob + KPS(lds_r100_off) + 8 * kRewardCSlot, U);
     } else if (!cur_ok) {  // no pair for this wave: its part of the flushes only (the same
                            // barriers as the waves with pairs: DETECT as theirs)
       for (int i0 = 0; i0 < nsteps; i0 += stage_rows) {
         flush_staged2<PIPE>(out, sw + (dbl ? 2 * hcur * wrows : 0), kp.E, e0, traj ? i0 : 0,
-                            min(stage_rows, nsteps - i0), lower, NWG, !dbl, &kp, tb.util, U);
+                            min(stage_rows, nsteps - i0), lower, NWG, !dbl,
+                            lblob + KPS(lds_r100_off) + 8 * kRewardCSlot, U);
         if (dbl) hcur ^= 1;
       }
     }
@@ -3038,6 +3186,15 @@ struct BlockRow {
   int t_after, nact, ncon;
 };
 
+// The block row's exact mean (block_finish_row_lean's rare path; wave-wide, lane 63 holds it)
+MEV_GUARD_FN float block_fix_row(const float* rates, int U, int lane, const char* rc, int nact) {
+  const RewardC c = reward_c(rc);
+  long long v = 0;
+#pragma unroll 1
+  for (int u = lane; u < U; u += 64) v += util_fix50c(rint((double)rates[4 * u] * 100.0), c);
+  return exact_mean50(seg_lsum_rows<64>(v), nact);
+}
+
 template <bool LEAN>
 __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& out,
                                                  const double* ps, const int* wt, int nw, int e,
@@ -3080,7 +3237,7 @@ __device__ __forceinline__ void block_finish_row(const KParams& kp, const KOut& 
 __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const KOut& out,
                                                       const double* ps, int nw, int e, int row,
                                                       const BlockRow& r, int lane, bool fix,
-                                                      const double* __restrict__ utab) {
+                                                      const char* rc) {
   const double su = wave_sum_f64(lane < nw ? ps[lane] : 0.0);
   // reward_risky (rare, wave-uniform): the exact mean from the row's obs rates, which every wave
   // stored before the barrier this one follows (fenced: __syncthreads); `fix`: the row is still
@@ -3089,15 +3246,13 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
   float exact = 0.f;
   const float sum_f = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
                                                     __builtin_bit_cast(int, (float)su), 63));
-  const bool risky = fix && reward_risky(sum_f * 0x1p-24f, r.nact, 0x1p-24f, kp);
-  if (risky) {  // (rolled, the pointers laundered inside the branch: see flush_staged2)
+  const bool risky = fix && reward_risky_c(sum_f * 0x1p-24f, r.nact, 0x1p-24f,
+                                            *reinterpret_cast<const float*>(rc + 24));
+  if (risky) {  // (the pointer laundered inside the branch: see flush_staged2)
     const float* obs_f = reinterpret_cast<const float*>(out.obs);
-    asm volatile("" : "+s"(obs_f), "+s"(utab));
-    const float* rates = obs_f + 4 * ((size_t)row * kp.E + (size_t)e) * (size_t)kp.U + 2;
-    long long v = 0;
-#pragma unroll 1
-    for (int u = lane; u < kp.U; u += 64) v += util_fix50(rint((double)rates[4 * u] * 100.0), true, kp, utab);
-    exact = exact_mean50(seg_lsum_rows<64>(v), r.nact);
+    asm volatile("" : "+s"(obs_f));
+    exact = block_fix_row(obs_f + 4 * ((size_t)row * kp.E + (size_t)e) * (size_t)kp.U + 2, kp.U,
+                          lane, rc, r.nact);
   }
   if (lane == 63) {
     // the float32 reward as the packed kernels' lean path forms it (a float32 product with the
@@ -3145,6 +3300,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   extern __shared__ __align__(16) char lds_raw[];
   // (a scenario instance: its station count; LDS for four workgroups per CU with two UEs per lane)
   __shared__ __align__(16) int2 lds_keys[SCN ? scn_const(SCN).B + 2 : kMaxB + 2 + kMaxClasses];
+  __shared__ __align__(8) double lds_rc[4];  // (lean) RewardC, written in the prologue
   const int tid = threadIdx.x;
   const int nt = blockDim.x;
   const int U = KPS(U);
@@ -3250,6 +3406,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                     (unsigned)i));
     }
     for (int i = tid; i < KPS(B); i += nt) L.cnt[i] = 0;  // step 0's counts
+    if (LEAN && tid == 0) {
+      *reinterpret_cast<const double**>(&lds_rc[0]) = tb.util;
+      lds_rc[1] = kp.util_sat;
+      lds_rc[2] = (double)kp.util_kmax;
+      *reinterpret_cast<float*>(&lds_rc[3]) = kp.u_err;
+    }
     if (CULL && tid == 0) lds_keys[nb] = make_int2(0, -1);  // the candidate lists' padding slot
     // the slot holds the state after the env's last draw: the state row without a table, or
     // after draws past it (mev_state.pcg)
@@ -3593,7 +3755,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       // step's barrier)
       if (LEAN ? (w == 0 && i > 0) : (tid == 0 && i > 0)) {
         const double* pps = L.ps + 64 * (par ^ 1);
-        if (LEAN) block_finish_row_lean(kp, out, pps, nv, e, traj ? i - 1 : 0, prev, lane, traj != 0, tb.util);
+        if (LEAN) block_finish_row_lean(kp, out, pps, nv, e, traj ? i - 1 : 0, prev, lane, traj != 0,
+                                        reinterpret_cast<const char*>(lds_rc));
         else block_finish_row<LEAN>(kp, out, pps, L.wt + 64 * (par ^ 1), nv, e, traj ? i - 1 : 0, prev);
       }
       prev = BlockRow{t + 1, nact, ncon};
@@ -3604,7 +3767,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     __syncthreads();  // the last step's partial sums
     if (LEAN ? (w == 0 && nsteps > 0) : (tid == 0 && nsteps > 0)) {
       const int lp = (nsteps - 1) & 1;  // the last step's parity
-      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev, lane, true, tb.util);
+      if (LEAN) block_finish_row_lean(kp, out, L.ps + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev, lane, true,
+                                      reinterpret_cast<const char*>(lds_rc));
       else block_finish_row<LEAN>(kp, out, L.ps + 64 * lp, L.wt + 64 * lp, nv, e, traj ? nsteps - 1 : 0, prev);
     }
     // ---- epilogue: the state after the last step ----------------------------------------
@@ -3886,8 +4050,12 @@ __device__ __forceinline__ uint32_t het_rank(const uint2* __restrict__ words, in
 // and per (UE class cu, station j) the pair's {offset, largest rank} into the blob at pk
 __global__ void k_het_info(const uint2* __restrict__ words, int nwords, int NB, int NU, int B,
                            const uint8_t* __restrict__ bs_cls, const int2* __restrict__ pair,
-                           int reach, int2* __restrict__ pk, int* __restrict__ info) {
+                           int reach, int2* __restrict__ pk, int* __restrict__ info,
+                           const int2* __restrict__ bs, uint32_t* __restrict__ st) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (st)  // (mode 6) station j: x | y << 12 | class << 24
+    for (int j = 0; j < B; ++j)
+      st[j] = ((uint32_t)bs[j].x & 4095u) | (((uint32_t)bs[j].y & 4095u) << 12) | ((uint32_t)bs_cls[j] << 24);
   int off = 0;
   for (int cu = 0; cu < NU; ++cu)
     for (int cb = 0; cb < NB; ++cb) {
@@ -3911,9 +4079,18 @@ __global__ void k_het_map(const int2* __restrict__ cellv, int cells, const uint2
                           int nwords, int reach, int NB, int NU, const uint8_t* __restrict__ bs_cls,
                           const int2* __restrict__ pair, const double* __restrict__ rate_full,
                           const int* __restrict__ info, uint8_t* __restrict__ blob, int rate_off,
-                          int rate_cap) {
+                          int rate_cap, int nib) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cells) {
+  if (nib && 2 * i < cells) {  // (mode 6) s* per cell, 4 bits, two cells a byte
+    uint32_t v = 0;
+    for (int h = 0; h < 2; ++h) {
+      const int cl = 2 * i + h;
+      const int sx = cl < cells ? cellv[cl].x : -1;
+      v |= (uint32_t)(sx < 0 ? 15 : sx) << (4 * h);
+    }
+    blob[i] = (uint8_t)v;
+  }
+  if (!nib && i < cells) {
     const int2 v = cellv[i];
     uint32_t ent = 0xF000u;  // nothing within any pair's reach
     if (v.x >= 0) {
@@ -4059,6 +4236,7 @@ struct mev_ctx {
   // rate count read back like mode 3's |D|, through dcount_pin); het_lds 0: packed kernels only
   int het_lds;
   int het_reach, het_nwords, het_r100_off, het_st_off, het_rate_off, het_rate_cap, het_cus;
+  int het_nib_st, het_words_off;  // (mode 6) station words, rank indices
   int2* het_cell;
   uint8_t* het_flag;
   uint2* het_words;
@@ -4571,11 +4749,19 @@ static int build_het_lds(mev_ctx* c) {
   c->het_lds = 0;
   const size_t cells = (size_t)c->p.width * c->p.height;
   if (!c->het_packed || c->p.two_groups < 0 || c->p.lds_tables < 0 || !(kp.U == 15 || kp.U == 30) ||
-      kp.B > 15 || kp.tab_m <= 0 || cells >= 65536 || c->d2max < 0)
+      kp.B > 15 || kp.tab_m <= 0 || cells >= 65536 || c->d2max < 0 ||
+      (kHetNib && (c->p.width > 4096 || c->p.height > 4096)))
     return MEV_OK;
   const int NB = kp.nb_cls, NU = kp.nu_cls;
-  const size_t r100_off = up16(2 * cells), st_off = r100_off + 8 * 72;
-  const size_t rate_off = up16(st_off + 8 * (size_t)NU * kp.B);
+  const size_t nwords = (size_t)c->d2max / 32 + 1;
+  // mode 6: [0, nib) 4-bit s* per cell; [st, +64) station x | y << 12 | class << 24; [pk,
+  // +8 NU B) pairs; [words, +8 NB (nwords + 1)) the classes' rank indices; [r100, +576); rates.
+  // mode 5: [0, 2 cells) u16 entries; [r100, +576); [pk = st_off, +8 NU B); rates.
+  const size_t nib_bytes = up16((cells + 1) / 2);
+  const size_t pk6 = nib_bytes + 64, words6 = up16(pk6 + 8 * (size_t)NU * kp.B);
+  const size_t r100_off = kHetNib ? up16(words6 + 8 * (size_t)NB * (nwords + 1)) : up16(2 * cells);
+  const size_t st_off = kHetNib ? pk6 : r100_off + 8 * 72;  // (the pairs' table)
+  const size_t rate_off = kHetNib ? up16(r100_off + 8 * 72) : up16(st_off + 8 * (size_t)NU * kp.B);
   const size_t one_wave = lds2_per_wave(kp.envs_per_wave, kp.B, kp.tab_m, 1) +
                           (size_t)2 * kp.envs_per_wave * kStage2Bytes + 4;
   if (rate_off + one_wave + 8 * 64 > (size_t)kLds2BytesPerWG) return MEV_OK;
@@ -4590,7 +4776,8 @@ static int build_het_lds(mev_ctx* c) {
       hipMalloc(&c->het_blob, rate_off + 8 * (size_t)cap) != hipSuccess)
     return MEV_ENOMEM;
   MEV_HIP(hipMemset(c->het_blob, 0, rate_off + 8 * (size_t)cap));
-  MEV_HIP(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(c->het_blob), 0xF000, cells));
+  if (kHetNib) MEV_HIP(hipMemset(c->het_blob, 0xff, (cells + 1) / 2));  // no station until a layout
+  else MEV_HIP(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(c->het_blob), 0xF000, cells));
   double r100[72] = {0.0};
   for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
   MEV_HIP(hipMemcpy(c->het_blob + r100_off, r100, sizeof(r100), hipMemcpyHostToDevice));
@@ -4598,6 +4785,8 @@ static int build_het_lds(mev_ctx* c) {
   MEV_HIP(hipMemcpy(c->het_info, &zero, sizeof(int), hipMemcpyHostToDevice));
   c->het_r100_off = (int)r100_off;
   c->het_st_off = (int)st_off;
+  c->het_nib_st = (int)nib_bytes;
+  c->het_words_off = (int)words6;
   c->het_rate_off = (int)rate_off;
   c->het_rate_cap = cap;
   MEV_HIP(hipDeviceGetAttribute(&c->het_cus, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -4863,6 +5052,21 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
       c->kp.util_direct = 1;
     }
   }
+  // the reward guard's constants (RewardC) in the r100 tables' spare slots of the LDS blobs
+  if (c->util) {
+    struct {
+      const double* tab;
+      double sat, kmax;
+      float u_err, pad;
+    } rc{c->util, c->kp.util_sat, (double)c->kp.util_kmax, c->kp.u_err, 0.f};
+    static_assert(sizeof(rc) == 32, "RewardC: four 8-byte slots");
+    if (c->blob && c->kp.lds_mode >= 1)
+      MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + c->kp.lds_r100_off + 8 * kRewardCSlot, &rc,
+                        sizeof(rc), hipMemcpyHostToDevice));
+    if (c->het_blob)
+      MEV_HIP(hipMemcpy(c->het_blob + c->het_r100_off + 8 * kRewardCSlot, &rc, sizeof(rc),
+                        hipMemcpyHostToDevice));
+  }
   // ---- launch shape of mev_step: one kernel per step (auto), or on request two halves on
   //      two streams (measured 3-5 % faster at 65536 large envs, but the overlapping
   //      dispatches cannot be timed one by one)
@@ -5113,10 +5317,11 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
     if (c->het_lds && lean && traj && pre_ok && c->p.two_groups >= 0 && c->p.two_groups <= 2) {
       const int nrate = layout_dcount(c);
       if (nrate >= 0 && nrate <= c->het_rate_cap) {
-        // one group per wavefront unless two_groups = 1: at 65,536 mobile-large-mixed envs 2.95 vs
-        // 4.04 ms per 200-step launch (the tables leave room for ~10 two-group waves per
-        // workgroup, 2.5 per SIMD, against 16 one-group waves)
-        const int R = c->p.two_groups == 1 ? 2 : 1;
+        // mode 6 (the 4-bit station map: 92 KB of tables on the large layout): two groups per
+        // wavefront unless two_groups = 2 -- at 65,536 mobile-large-mixed envs 2.93 vs 3.29 ms
+        // per 200-step launch; mode 5 (u16 entries, 136 KB: ~10 two-group waves per workgroup):
+        // one group unless two_groups = 1 -- 2.93 vs 4.05 ms (interleaved on one box)
+        const int R = c->p.two_groups == 1 ? 2 : c->p.two_groups == 2 ? 1 : kHetNib ? 2 : 1;
         const int G = kp.envs_per_wave;
         const int units = R == 2 ? pairs : groups;
         const size_t blob = ((size_t)c->het_rate_off + 8 * (size_t)nrate + 15) & ~(size_t)15;
@@ -5150,9 +5355,11 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
           }
           const int blocks = std::min((units + nw2 - 1) / nw2, c->het_cus * c->het_occ_n);
           KParams kp5 = kp;
-          kp5.lds_mode = 5;
+          kp5.lds_mode = kHetNib ? 6 : 5;
           kp5.lds_assoc = (int)blob;
-          kp5.lds_st_off = c->het_st_off;
+          kp5.lds_st_off = kHetNib ? c->het_nib_st : c->het_st_off;
+          kp5.lds_r16_off = c->het_st_off;     // (mode 6: the pairs' table)
+          kp5.lds_rank_off = c->het_words_off;  // (mode 6)
           kp5.lds_rate_off = c->het_rate_off;
           kp5.lds_r100_off = c->het_r100_off;
           KTables tb5 = tb;
@@ -5422,12 +5629,17 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                            nd, c->het_words + (size_t)cb * (nw + 1), nw);
       hipLaunchKernelGGL(k_het_info, dim3(1), dim3(64), 0, s, c->het_words, nw, NB, NU,
                          c->p.num_bs, c->h_bcl, c->h_pair, reach,
-                         reinterpret_cast<int2*>(c->het_blob + c->het_st_off), c->het_info);
+                         reinterpret_cast<int2*>(c->het_blob + c->het_st_off), c->het_info,
+                         reinterpret_cast<const int2*>(bs_xy),
+                         kHetNib ? reinterpret_cast<uint32_t*>(c->het_blob + c->het_nib_st) : nullptr);
       const int n = std::max(cells, NB * nd);
       hipLaunchKernelGGL(k_het_map, dim3((n + 255) / 256), dim3(256), 0, s, c->het_cell, cells,
                          c->het_words, nw, reach, NB, NU, c->h_bcl, c->h_pair, c->rate_full,
-                         c->het_info, c->het_blob, c->het_rate_off, c->het_rate_cap);
+                         c->het_info, c->het_blob, c->het_rate_off, c->het_rate_cap, kHetNib ? 1 : 0);
       MEV_HIP(hipGetLastError());
+      if (kHetNib)  // the classes' rank indices into the blob
+        MEV_HIP(hipMemcpyAsync(c->het_blob + c->het_words_off, c->het_words,
+                               sizeof(uint2) * (size_t)NB * (nw + 1), hipMemcpyDeviceToDevice, s));
       MEV_HIP(hipMemcpyAsync(c->dcount_pin, c->het_info, sizeof(int), hipMemcpyDeviceToHost, s));
       MEV_HIP(hipEventRecord(c->ev_dcount, s));
       c->dcount_pending = 1;
