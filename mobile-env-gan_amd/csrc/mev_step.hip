@@ -636,10 +636,12 @@ __device__ __forceinline__ bool reward_risky_c(float sum, int nact, float q, flo
 __device__ __forceinline__ float exact_mean50(long long s, int nact) {
   return (float)((double)s * 0x1p-50 / (double)nact);
 }
-// The guard's rare work out of line under MEV_GUARD_CALL: one copy of the code, whose scalars
-// then do not compete with the step loops' (inlined into a loop, they kept kernel arguments
-// live across it and spilled others to VGPR lanes).
-#ifdef MEV_GUARD_CALL
+// The guard's rare work out of line: one copy of the code, whose scalars then do not compete
+// with the step loops' (inlined into a loop, they kept kernel arguments live across it and
+// spilled others to VGPR lanes).
+// (default; -DMEV_GUARD_INLINE for the A/B: at 4,096 medium envs 92.8 vs 99.4 us per 200-step
+// launch, interleaved on one box)
+#ifndef MEV_GUARD_INLINE
 #define MEV_GUARD_FN __device__ __attribute__((noinline))
 #else
 #define MEV_GUARD_FN __device__ __forceinline__
@@ -1329,6 +1331,7 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
                        reward_risky_c(ISUM ? (float)isum_u * 0x1p-25f : (float)sum_u, nact,
                                       ISUM ? 0x1p-25f : 0.f, u_err);
     if (bal(risky)) {
+      wait_vmem();  // (no load in flight across the call)
       const RewardC c = LDSA ? reward_c(rcp)
                              : RewardC{tb.util, kp.util_sat, (double)kp.util_kmax, kp.u_err};
       const float ex = packed_fix<ROWS, PC>(active ? cents : -1.0, U, u, c.tab, c.kmax, c.sat, nact);
@@ -2127,13 +2130,26 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // than the env's last write into two words of their env's histogram instead (no branch;
     // re-zeroed next step; min(): never past the env's area)
     const bool lead = klead < nok[r];
-    // (reward_risky, rare: the exact reward's float32 bits instead, flag 0x100)
-    const bool risky = lead && reward_risky((float)isum * 0x1p-25f, nact, 0x1p-25f, kp);
+    // (reward_risky, rare: the exact reward's float32 bits instead, flag 0x100; the constants
+    // from the blob's RewardC)
+    const char* rcp = lblob + KPS(lds_r100_off) + 8 * kRewardCSlot;
+#ifdef MEV_NO_STEP_GUARD  // (dev A/B only: the two-group step without the guard)
+    const bool risky = false;
+#else
+    const bool risky = lead && reward_risky_c((float)isum * 0x1p-25f, nact, 0x1p-25f,
+                                              *reinterpret_cast<const float*>(rcp + 24));
+#endif
     int word0 = isum, flag = 0;
     if (bal(risky)) {
-      const long long se = seg_lsum_rows<PC>(util_fix50((double)cf[r], active[r], kp, tb.util));
+      // (every load landed before the call: the next pair's prefetch registers are not tracked
+      // by the compiler, and a callee's save / restore of one in flight would lose its data;
+      // tools/check_prefetch_regs.py checks the wait)
+      wait_vmem();
+      const RewardC rc = reward_c(rcp);
+      const float ex = packed_fix<true, PC>(active[r] ? (double)cf[r] : -1.0, U, u, rc.tab, rc.kmax,
+                                            rc.sat, nact);
       if (risky) {
-        word0 = __float_as_int(exact_mean50(se, nact));
+        word0 = __float_as_int(ex);
         flag = 0x100;
       }
     }
@@ -2480,6 +2496,7 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
     const float* obs_f = reinterpret_cast<const float*>(out.obs);
     float* rew = out.reward;
     asm volatile("" : "+s"(obs_f), "+s"(rew));
+    wait_vmem();  // (see lds2_step: no prefetch in flight across the call)
     flush_fix(srow, obs_f, rew, rc, E, e0, row0, nr, NWG, U);
   }
   if (trailing) lds_barrier();
@@ -3251,6 +3268,7 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
   if (risky) {  // (the pointer laundered inside the branch: see flush_staged2)
     const float* obs_f = reinterpret_cast<const float*>(out.obs);
     asm volatile("" : "+s"(obs_f));
+    wait_vmem();  // (no load in flight across the call)
     exact = block_fix_row(obs_f + 4 * ((size_t)row * kp.E + (size_t)e) * (size_t)kp.U + 2, kp.U,
                           lane, rc, r.nact);
   }

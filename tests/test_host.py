@@ -382,6 +382,14 @@ def test_prefetch_registers_check_on_generated_assembly():
     assert cp.violations(cond)[0]
     both = head + "\ts_cbranch_scc1 .LBB0_2\n\tds_read_u8 v1, v0\n.LBB0_2:\n" + tail
     assert cp.violations(both) == ([], 1)  # (no path reads it)
+    # a call (the reward guard's out-of-line rare path) while a prefetch is in flight: flagged
+    # unless an s_waitcnt vmcnt(0) precedes it in its block (the callee's register save /
+    # restore would lose the landing data)
+    call = ("_Zk:\n\tglobal_load_dword v5, v[2:3], off ; mev-prefetch\n; %bb.1:\n"
+            "\ts_swappc_b64 s[30:31], s[0:1]\n\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v5\n")
+    assert cp.violations(call)[0]
+    waited = call.replace("; %bb.1:\n", "; %bb.1:\n\ts_waitcnt vmcnt(0)\n")
+    assert cp.violations(waited) == ([], 1)
     text = open(cp.build_asm()).read()
     v, n = cp.violations(text)
     assert n >= 8 and v == []

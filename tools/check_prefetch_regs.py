@@ -11,7 +11,9 @@ data landed) and no spill. This check, per kernel with prefetch loads:
     range -- a copy at a loop edge -- shows as a tied register that no load wrote);
   * no instruction between a prefetch load and the next wait in the code reads one of the
     loaded registers (copies, spills, any use), other than further prefetch loads;
-  * no instruction between them writes one (a register reused while the load is in flight).
+  * no instruction between them writes one (a register reused while the load is in flight);
+  * no call (s_swappc / s_call) while one is in flight, unless an s_waitcnt vmcnt(0) precedes
+    it in its block: the callee's save / restore of a register it uses would lose the data.
 
 python tools/check_prefetch_regs.py [file.s]   (default: builds `make asm` and checks it)
 """
@@ -109,6 +111,7 @@ def check_kernel(name: str, lines):
     bad = []
     loaded, tied = set(), set()
     inflight = set()  # registers of loads issued since the last wait
+    vm_waited = False  # an s_waitcnt vmcnt(0) earlier in the current block
     for idx, (no, text) in enumerate(lines):
         if "; mev-prefetch-wait" in text:
             regs = regs_of(text.split("mev-prefetch-wait", 1)[1])
@@ -121,9 +124,15 @@ def check_kernel(name: str, lines):
             loaded |= dst
             inflight |= dst
             continue
+        code = text.split(";")[0]
+        if code.strip().endswith(":") or text.startswith("; %bb."):
+            vm_waited = False  # (a block starts: no wait of this block seen yet)
+        if "s_waitcnt" in code and "vmcnt(0)" in code:
+            vm_waited = True
+        if inflight and re.match(r"\s*s_(swappc|call)_b64", code) and not vm_waited:
+            bad.append((no, text.strip(), "call while prefetch register(s) are in flight"))
         if not inflight:
             continue
-        code = text.split(";")[0]
         if not code.strip() or code.strip().startswith(".") or code.strip().endswith(":"):
             continue
         op, ops = _split_operands(text)
