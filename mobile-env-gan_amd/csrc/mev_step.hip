@@ -75,6 +75,8 @@ struct KParams {
   int util_kmax;      // utility table covers rounded rates k/100 for k in [0, util_kmax]
   int util_direct;    // 1: evaluate the utility in-kernel (no monotone saturation point)
   float u_err;        // bound on |float32 utility (utility_f32r) - float64 utility| (reward_risky)
+  float r_thr;        // reward_risky as a bound on the fast mean: |mean| <= r_thr (host, from u_err)
+  int r_thr25;        // ... on the 2^-25 fixed-point sum: |isum| <= nact r_thr25
   int hist_lds;       // packed shape: per-env BS counts in an LDS histogram ([G][B] per wave)
   int tab_m;          // episode draw table: pairs per env (0: off)
   float inv_w, inv_h; // obs normalisation
@@ -593,30 +595,24 @@ __device__ __forceinline__ int seg_isum_rows(int x) {
 // (metrics.py:25-28). The lean kernels sum float32 utilities, each within kp.u_err of the
 // float64 value (the host's bound for the utility parameters), as fixed point (quantum q per
 // UE); that mean is within 1e-5 unless the sum is small against its error bound --
-// nact (u_err + q) >= 9.5e-6 |sum|: mean utilities near zero, cancellation (none in the
-// registered large / medium / mixed workloads; ~1 % of small's env-steps). Such an env's reward
-// comes from the exact float64 utilities (the device table tb.util by cents, utility_of) summed
-// as 2^-50 fixed point in int64: associative, so every kernel shape forms the same bits.
-__device__ __forceinline__ bool reward_risky(float sum, int nact, float q, const KParams& kp) {
-  return nact > 0 && fabsf(sum) * 9.5e-6f <= (float)nact * (kp.u_err + q);
-}
-__device__ __forceinline__ long long util_fix50(double cents, bool take, const KParams& kp,
-                                                const double* __restrict__ tab) {
-  if (!take) return 0;
-  const double uu = cents <= (double)kp.util_kmax ? tab[(int)cents] : kp.util_sat;
-  return (long long)(uu * 0x1p50);
-}
-// The guard's constants held in LDS where a kernel's scalar registers are scarce (read only by
-// the rare path and the flush's test): {utility table, util_sat, util_kmax, u_err} as four
-// 8-byte slots -- the r100 table's slots 66..69 of the LDS blobs (kRewardCSlot), or a static
-// array of the block kernel. Loop-invariant kernel arguments used there were kept in SGPRs
-// across the step loops and spilled others to VGPR lanes (+9 % at 4,096 medium envs).
+// nact (u_err + q) >= 9.5e-6 |sum|, tested as |mean| <= kp.r_thr or |isum| <= nact kp.r_thr25
+// (host-computed: one compare where the sum is formed): mean utilities near zero, cancellation
+// (none in the registered large / medium / mixed workloads; ~1 % of small's env-steps). Such an
+// env's reward comes from the exact float64 utilities (the device table tb.util by rounded rate,
+// the non-lean kernels' values) summed as 2^-50 fixed point in int64: associative, so every
+// kernel shape forms the same bits.
+// The rare path's constants are held in LDS where a kernel's scalar registers are scarce:
+// {utility table, util_sat, util_kmax, u_err | r_thr25} as four 8-byte slots -- the r100 table's
+// slots 66..69 of the LDS blobs (kRewardCSlot), or a static array of the block kernel (kernel
+// arguments used there were kept in SGPRs across the step loops and spilled others to VGPR
+// lanes: +9 % at 4,096 medium envs).
 constexpr int kRewardCSlot = 66;
 struct RewardC {
   const double* tab;
   double sat;
   double kmax;
   float u_err;
+  int thr25;  // KParams::r_thr25
 };
 __device__ __forceinline__ RewardC reward_c(const char* p) {  // (p: 8-byte aligned LDS)
   RewardC c;
@@ -624,14 +620,12 @@ __device__ __forceinline__ RewardC reward_c(const char* p) {  // (p: 8-byte alig
   c.sat = *reinterpret_cast<const double*>(p + 8);
   c.kmax = *reinterpret_cast<const double*>(p + 16);
   c.u_err = *reinterpret_cast<const float*>(p + 24);
+  c.thr25 = *reinterpret_cast<const int*>(p + 28);
   return c;
 }
 __device__ __forceinline__ long long util_fix50c(double cents, const RewardC& c) {
   const double uu = cents <= c.kmax ? c.tab[(int)cents] : c.sat;
   return (long long)(uu * 0x1p50);
-}
-__device__ __forceinline__ bool reward_risky_c(float sum, int nact, float q, float u_err) {
-  return nact > 0 && fabsf(sum) * 9.5e-6f <= (float)nact * (u_err + q);
 }
 __device__ __forceinline__ float exact_mean50(long long s, int nact) {
   return (float)((double)s * 0x1p-50 / (double)nact);
@@ -939,7 +933,7 @@ __device__ __forceinline__ void flush_pending(const KOut& out, const Pending& p,
 template <bool ROWS, int PC>
 MEV_GUARD_FN float packed_fix(double cents, int U, int u, const double* tab, double kmax,
                               double sat, int nact) {
-  const long long v = cents < 0.0 ? 0 : util_fix50c(cents, RewardC{tab, sat, kmax, 0.f});
+  const long long v = cents < 0.0 ? 0 : util_fix50c(cents, RewardC{tab, sat, kmax, 0.f, 0});
   const long long se = ROWS ? seg_lsum_rows<PC>(v) : seg_lsum(v, U, u);
   return exact_mean50(se, nact);
 }
@@ -1324,16 +1318,15 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   bool use_exact = false;
   float exact_r = 0.f;
   if constexpr (LEAN) {
-    // (the constants from the LDS blob's RewardC where there is one)
+    // (the rare path's constants from the LDS blob's RewardC where there is one)
     const char* rcp = LDSA ? lblob + KPS(lds_r100_off) + 8 * kRewardCSlot : nullptr;
-    const float u_err = LDSA ? *reinterpret_cast<const float*>(rcp + 24) : kp.u_err;
-    const bool risky = env_ok && leader &&
-                       reward_risky_c(ISUM ? (float)isum_u * 0x1p-25f : (float)sum_u, nact,
-                                      ISUM ? 0x1p-25f : 0.f, u_err);
+    const bool risky = env_ok && leader && nact > 0 &&
+                       (ISUM ? (uint32_t)abs(isum_u) <= (uint32_t)nact * (uint32_t)kp.r_thr25
+                             : fabsf((float)sum_u) <= (float)nact * kp.r_thr);
     if (bal(risky)) {
       wait_vmem();  // (no load in flight across the call)
       const RewardC c = LDSA ? reward_c(rcp)
-                             : RewardC{tb.util, kp.util_sat, (double)kp.util_kmax, kp.u_err};
+                             : RewardC{tb.util, kp.util_sat, (double)kp.util_kmax, kp.u_err, 0};
       const float ex = packed_fix<ROWS, PC>(active ? cents : -1.0, U, u, c.tab, c.kmax, c.sat, nact);
       use_exact = risky;
       exact_r = ex;
@@ -2136,8 +2129,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
 #ifdef MEV_NO_STEP_GUARD  // (dev A/B only: the two-group step without the guard)
     const bool risky = false;
 #else
-    const bool risky = lead && reward_risky_c((float)isum * 0x1p-25f, nact, 0x1p-25f,
-                                              *reinterpret_cast<const float*>(rcp + 24));
+    const bool risky = lead && nact > 0 && (uint32_t)abs(isum) <= (uint32_t)nact * (uint32_t)kp.r_thr25;
 #endif
     int word0 = isum, flag = 0;
     if (bal(risky)) {
@@ -2450,7 +2442,9 @@ MEV_GUARD_FN void flush_fix(const int* srow, const float* obs_f, float* rew, con
     const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
     const uint32_t b = (uint32_t)v.y;
     const int nact = (int)(b & 0x7fu);
-    if ((b & 0x100u) || !reward_risky_c((float)v.x * 0x1p-25f, nact, 0x1p-25f, c.u_err)) continue;
+    if ((b & 0x100u) || !(nact > 0 && fabsf((float)v.x * 0x1p-25f) * 9.5e-6f <=
+                                          (float)nact * (c.u_err + 0x1p-25f)))
+      continue;
     const float* rates = obs_f + 4 * ((size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)) * (size_t)U + 2;
     long long su = 0;
 #pragma unroll 1
@@ -2473,6 +2467,8 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
   lds_barrier();
   const float inv_nwg = 1.0f / (float)NWG;
   bool any = false;
+  // (the test in float32 against u_err: 92.5 vs 95.5 us per 200-step launch at 4,096 medium envs
+  // for the integer form against r_thr25, interleaved on one box)
   const float u_err = DETECT ? *reinterpret_cast<const float*>(rc + 24) : 0.f;
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     // q / NWG through float (q + 1/2 is >= 1/2 away from a multiple of NWG; exact for q < 2^22)
@@ -2488,7 +2484,9 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
           (b & 0x100u) ? __int_as_float(v.x)
                        : nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
       at(out.done + ro, o) = (uint8_t)((b >> 7) & 1u);
-      if (DETECT) any = any || (!(b & 0x100u) && reward_risky_c((float)v.x * 0x1p-25f, nact, 0x1p-25f, u_err));
+      if (DETECT)
+        any = any || (!(b & 0x100u) && nact > 0 &&
+                      fabsf((float)v.x * 0x1p-25f) * 9.5e-6f <= (float)nact * (u_err + 0x1p-25f));
     }
   }
   if (DETECT && __syncthreads_or(any)) {  // rare
@@ -3263,8 +3261,7 @@ __device__ __forceinline__ void block_finish_row_lean(const KParams& kp, const K
   float exact = 0.f;
   const float sum_f = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
                                                     __builtin_bit_cast(int, (float)su), 63));
-  const bool risky = fix && reward_risky_c(sum_f * 0x1p-24f, r.nact, 0x1p-24f,
-                                            *reinterpret_cast<const float*>(rc + 24));
+  const bool risky = fix && r.nact > 0 && fabsf(sum_f * 0x1p-24f) <= (float)r.nact * kp.r_thr;
   if (risky) {  // (the pointer laundered inside the branch: see flush_staged2)
     const float* obs_f = reinterpret_cast<const float*>(out.obs);
     asm volatile("" : "+s"(obs_f));
@@ -4934,6 +4931,12 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
       kp.u_err = (float)(2.0 * (A * ((3.0 * 0x1p-24 + 2.2e-8) / log(2.0) + 0x1p-22 * lmax) +
                                0x1p-22 * (1.0 + off + sc)));
       if (params->reward_exact > 0) kp.u_err = INFINITY;  // (every row takes the exact path)
+      // |sum| 9.5e-6 <= nact (u_err + q) as bounds on the mean (q = 2^-24, the coarser fixed
+      // point; 0.1 % wider): |mean| <= r_thr, and on the 2^-25 sum |isum| <= nact r_thr25, unsigned
+      // (every |isum| <= nact 2^25 <= 2^31: the caps take every row in reward_exact)
+      const double thr = (kp.u_err + 0x1p-24) / 9.5e-6 * 1.001;
+      kp.r_thr = (float)std::min(thr, 4.0);
+      kp.r_thr25 = (int)std::min(std::ceil(thr * 0x1p25), (double)(1 << 25));
     }
   }
 
@@ -5075,8 +5078,9 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     struct {
       const double* tab;
       double sat, kmax;
-      float u_err, pad;
-    } rc{c->util, c->kp.util_sat, (double)c->kp.util_kmax, c->kp.u_err, 0.f};
+      float u_err;
+      int thr25;
+    } rc{c->util, c->kp.util_sat, (double)c->kp.util_kmax, c->kp.u_err, c->kp.r_thr25};
     static_assert(sizeof(rc) == 32, "RewardC: four 8-byte slots");
     if (c->blob && c->kp.lds_mode >= 1)
       MEV_HIP(hipMemcpy(reinterpret_cast<char*>(c->blob) + c->kp.lds_r100_off + 8 * kRewardCSlot, &rc,
