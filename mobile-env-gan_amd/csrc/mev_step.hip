@@ -4636,7 +4636,7 @@ int64_t mev_build_rate_table(const mev_params* p, double* dst, int64_t cap) {
 // Movement parameters of a velocity (host IEEE float64 == device): the arrival threshold
 // d2snap = largest integer d2 with sqrt(d2) <= velocity, axis-parallel exactness, the float32
 // fast path's velocity and tie band (move_ue_p).
-static MoveP host_move_params(double velocity, int W, int H) {
+static MoveP host_move_params(double velocity, int W, int H, bool v15 = true) {
   MoveP mp;
   mp.vel = velocity;
   mp.vel_f = (float)velocity;
@@ -4654,7 +4654,7 @@ static MoveP host_move_params(double velocity, int W, int H) {
   // (q = +-velocity within 5e-7 relative, far from a half-integer) gives it -- no axis branch
   if (velocity == floor(velocity) && velocity <= 0x1p20) mp.axis_exact = 0;
   // velocity 1.5 on maps up to 1024: the exact integer step (step_v15)
-  if (velocity == 1.5 && W <= 1024 && H <= 1024) mp.axis_exact = 2;
+  if (v15 && velocity == 1.5 && W <= 1024 && H <= 1024) mp.axis_exact = 2;
   return mp;
 }
 
@@ -4713,11 +4713,18 @@ static int build_het(mev_ctx* c) {
   all.push_back(0.0);  // (never indexed; keeps the buffer non-empty)
   // movement parameters per UE: its own velocity (ue_velocity), else its class's; distinct
   // velocities need no class (velocity only drives movement, movement.py:42-62)
+  // (the integer step of velocity 1.5, step_v15, only when every UE moves at 1.5: a wave of
+  // mixed velocities issues both movement paths, and the float32 path with its tie fallback is
+  // exact for 1.5 as for any velocity)
+  std::vector<double> vel(U);
+  bool all15 = true;
+  for (int u = 0; u < U; ++u) {
+    vel[u] = p->ue_velocity ? p->ue_velocity[u]
+             : p->ue_class_params ? p->ue_class_params[4 * ucl[u]] : p->velocity;
+    all15 = all15 && vel[u] == 1.5;
+  }
   std::vector<MoveP> mv(U);
-  for (int u = 0; u < U; ++u)
-    mv[u] = host_move_params(p->ue_velocity ? p->ue_velocity[u]
-                             : p->ue_class_params ? p->ue_class_params[4 * ucl[u]] : p->velocity,
-                             p->width, p->height);
+  for (int u = 0; u < U; ++u) mv[u] = host_move_params(vel[u], p->width, p->height, all15);
   // stations grouped by class, each segment padded to an even length (pairs of keys)
   std::vector<int16_t> perm;
   std::vector<int> seg(NB + 1, 0);
