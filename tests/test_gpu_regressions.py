@@ -174,3 +174,46 @@ def test_reward_exact_every_kernel_vs_oracle(case):
         np.testing.assert_allclose(eng.reward.cpu().numpy(), o["metrics"][:, 2].astype(np.float32),
                                    rtol=1.2e-7, atol=0, err_msg=f"one-step reward {s}")
     eng.close()
+
+
+def _u_err(lower, upper, w1, w2, w3):
+    """KParams::u_err as the host computes it (mev_step.hip, mev_create's utility section)."""
+    import math
+    A = abs(w1 * math.log(2.0) / math.log(w3) * (2.0 / (upper - lower)))
+    r_sat = math.exp(upper * math.log(w3) / w1) - w2
+    lmax = max(1.0, abs(math.log2(w2 + 0.01)), abs(math.log2(w2 + max(r_sat, 0.01))))
+    off = abs(-2.0 * lower / (upper - lower) - 1.0)
+    sc = max(abs(lower), abs(upper)) * 2.0 / (upper - lower)
+    return 2.0 * (A * ((3.0 * 2.0 ** -24 + 2.2e-8) / math.log(2.0) + 2.0 ** -22 * lmax)
+                  + 2.0 ** -22 * (1.0 + off + sc))
+
+
+@pytest.mark.parametrize("lower,upper,coeffs", [(-20.0, 20.0, (10.0, 0.0, 10.0)),
+                                                (-5.0, 8.0, (4.0, 0.5, 2.0))])
+def test_float32_utility_within_the_guards_bound(lower, upper, coeffs):
+    """The reward guard (reward_risky) rests on a bound u_err on the float32 utility's error
+    (utility_f32r: the hardware log2 taken as 2 ulp, every rounding counted, then doubled). On
+    every active UE of a lean 45-step rollout (the shipped scenario instance at the defaults, the
+    generic one at other utility parameters) the obs utility is within HALF that bound of the
+    oracle's float64 utility -- the factor-2 margin holds on the hardware."""
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS["large"]
+    E, n = 2048, 45
+    seeds = 31 + np.arange(E)
+    p = EngineParams(num_envs=E, num_ues=L["num_ues"], num_bs=len(L["bs"]), velocity=1.5,
+                     util_lower=lower, util_upper=upper, util_coeffs=coeffs)
+    eng = StepEngine(p, L["bs"], seeds, device="cuda")
+    tr = eng.rollout(n)
+    ob = OracleBatch(OracleParams(velocity=1.5, lower=lower, upper=upper, coeffs=coeffs), L["bs"],
+                     L["num_ues"], seeds)
+    worst = 0.0
+    for s in range(n):
+        o = ob.step()
+        u = tr.obs[s, ..., 3].cpu().numpy().astype(np.float64)
+        act = ~np.isnan(o["util"])
+        worst = max(worst, float(np.max(np.abs(u[act] - o["util"][act]))))
+    eng.close()
+    bound = _u_err(lower, upper, *coeffs)
+    assert worst <= bound / 2, (worst, bound)
