@@ -1,5 +1,6 @@
 #!/bin/bash
-# The packed kernels' exact-reward branch after the step's stores (late) against HEAD (cur):
+# Variants built first with tools/build_variant.sh (pre = before the guard, cur = HEAD, late =
+# the packed kernels' exact-reward branch after the step's stores):
 # the GPU tests on the in-tree library, then interleaved A/Bs (tools/ab.sh).
 set -o pipefail
 export TMPDIR=/tmp
