@@ -20,9 +20,10 @@ Contract (see DESIGN.md "Measurement"):
 * Warmup: W steps, and then more until ``--warmup-floor-s`` seconds of back-to-back launches
   have run (untimed; the chip reaches its steady clock -- a 5-step warmup would time a cold
   launch). ``warmup`` in the line is W as requested; ``warmup_executed`` what ran.
-* Timed region: barrier + synchronize, the K steps, and when N > 1 a synchronize and the single
-  final all-gather of the (reward, done) batch over RCCL, synchronize + barrier. value = N*E*K /
-  max-over-ranks time. Nothing else runs inside it (no event record). Inputs are resident in
+* Timed region: barrier + synchronize, then the clock runs over the K steps and, when N > 1, a
+  synchronize and the single final all-gather of the (reward, done) batch over RCCL, to the
+  synchronize after it; the trailing barrier is outside the window (timed on its own,
+  `distributed.trailing_barrier_ms`). value = N*E*K / max-over-ranks window. Nothing else runs inside it (no event record). Inputs are resident in
   HBM before timing starts. With N > 1 both collectives (final batch, obs) run once in the
   untimed warmup, so the timed gather is not the process's first; the line reports the timed
   gather's own wall time (`distributed.final_gather_ms`, its share of the window) and the
@@ -104,11 +105,16 @@ def chunk_plan(steps: int, chunk: int):
 
 
 def timed_run(issue, plan, sync, barrier, collective=None):
-    """The timed region: barrier + sync, every launch of `plan`, the final collective (if any),
-    sync + barrier. Nothing else happens inside it: no event is recorded (a launch's duration
-    is measured after the region, `launch_timing`). With a collective the launches are
-    synchronised before it, so that its share of the window is known (`final_gather_ms`).
-    Returns (wall s of the region, wall s to the end of the launches, wall s of the collective)."""
+    """The timed region: barrier + sync, then the clock runs over every launch of `plan` and the
+    final collective (if any), up to the sync after them. Nothing else happens inside it: no
+    event is recorded (a launch's duration is measured after the region, `launch_timing`). With a
+    collective the launches are synchronised before it, so that its share of the window is known
+    (`final_gather_ms`). The trailing barrier only lines the ranks up for what follows: it is
+    timed on its own and NOT part of the window (with N > 1 an RCCL barrier is an all-reduce plus
+    a sync, tens of us against a ~190 us 20-step window) -- each rank's window ends when its own
+    work and the gather have completed, and the line takes the max over ranks of that.
+    Returns (wall s of the window, wall s to the end of the launches, wall s of the collective,
+    wall s of the trailing barrier)."""
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -126,7 +132,7 @@ def timed_run(issue, plan, sync, barrier, collective=None):
     else:
         t_steps = t_end - t0
     barrier()
-    return time.perf_counter() - t0, t_steps, t_coll
+    return t_end - t0, t_steps, t_coll, time.perf_counter() - t_end
 
 
 def launch_timing(issue, n, reps, sync, make_event, isolated):
@@ -490,9 +496,10 @@ def main():
         if n not in launchers:
             launchers[n] = eng.launcher(n, traj)
     barrier = dist.barrier if world > 1 else (lambda: None)
-    elapsed, t_steps, t_gather = timed_run(issue, plan, sync, barrier,
-                                           collective if world > 1 else None)
+    elapsed, t_steps, t_gather, t_barrier = timed_run(issue, plan, sync, barrier,
+                                                      collective if world > 1 else None)
     elapsed = max_over_ranks(elapsed, device)
+    t_barrier = max_over_ranks(t_barrier, device)
     t_steps = max_over_ranks(t_steps, device)
     t_gather = max_over_ranks(t_gather, device) if t_gather is not None else None
     if "rd" in gathered:
@@ -609,6 +616,9 @@ def main():
             "distributed": ({"world_size_seen": dist.get_world_size(),
                              "backend": dist.get_backend(),
                              "final_gather_ms": t_gather * 1e3,
+                             "trailing_barrier_ms": t_barrier * 1e3,
+                             "window": "max over ranks of (end of the final gather - t0); the "
+                                       "trailing barrier is outside it (trailing_barrier_ms)",
                              "final_gather_share": t_gather / elapsed,
                              "value_steps_only": world * E * K / t_steps,
                              "warmup_gathers": warm_gathers,

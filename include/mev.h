@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 22
+#define MEV_ABI_VERSION 23
 
 #define MEV_OK 0
 #define MEV_EINVAL (-22)   /* bad parameters / shapes */
@@ -172,7 +172,10 @@ typedef struct mev_params {
    * float32 utilities; wherever that sum could miss the reference's float64 mean by more than
    * 1e-5 relative (mean utilities near zero: cancellation), the env's reward is re-formed from
    * the exact float64 utilities (reward_risky in mev_step.hip). 1: every reward that way (the
-   * float32 reward of the float64 mean -- slower; tests pin the exact path with it). */
+   * float32 reward of the float64 mean -- slower; tests pin the exact path with it). k <= -2
+   * (tests): the risk band k times wider, so that a subset of rows takes the exact path. Every
+   * kernel shape decides with the same test (the 2^-25 fixed-point sum against nact r_thr25),
+   * so one env-step's reward has the same bits whichever shape ran it. */
   int32_t reward_exact;
 } mev_params;
 
@@ -202,6 +205,12 @@ typedef struct mev_ctx mev_ctx;
 
 /* Library ABI version (MEV_ABI_VERSION). */
 int mev_abi_version(void);
+
+/* Hash of the sources this library was compiled from (the first 16 hex digits of the SHA-256
+ * of csrc/mev_step.hip followed by include/mev.h; "unknown" for a build without the Makefile's
+ * -DMEV_SRC_HASH). The Python host compares it with the sources next to the library and refuses
+ * a stale build. No reference counterpart (build provenance). */
+const char* mev_source_hash(void);
 
 /* Build a context on the current HIP device: validates params, uploads the channel table
  * (Okumura-Hata -> SNR -> Shannon rate at every integer squared distance,

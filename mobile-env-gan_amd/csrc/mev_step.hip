@@ -104,6 +104,10 @@ struct KParams {
   // cull_nc in all (block_cull_params)
   int cull_log, cull_nx, cull_nc;
   int st8;            // compact UE state: uint8 x4 per UE (maps <= 255 per side; 255 = -1)
+  // 1: the float32 utility cannot hold 1e-5 relative near zero (a nonzero scaled offset or w2:
+  // ur * scale + offset / log2(w2 + r) cancel) -- the utility comes from the exact table instead
+  // (non-lean kernels); 0 for the reference's default parameters (offset 0, w2 0)
+  int util_exact;
 };
 
 struct KState {
@@ -964,7 +968,8 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   const uint64_t segmask = m.segmask, lt = m.lt;
   const bool want_metrics = !LEAN && out.metrics != nullptr;
   const bool want_qoe = !LEAN && out.qoe_stats != nullptr;
-  const bool exact_util = !LEAN && (out.util64 != nullptr || kp.util_direct || want_qoe);
+  const bool exact_util =
+      !LEAN && (out.util64 != nullptr || kp.util_direct || kp.util_exact || want_qoe);
   const bool want_rate = !LEAN && (out.rate64 != nullptr || want_metrics || exact_util);
   const size_t idx = (size_t)e * U + u;
   int t = cur.t;
@@ -1728,13 +1733,6 @@ __host__ __device__ constexpr int lds2_hist_stride(int G, int B) {
 // drawn = M + 1. Measured: the flag-free form 101 vs 104 us per 200-step launch at 4,096 medium
 // envs, but 1.55 vs 1.51 ms at 65,536 large envs in the two-group loop, interleaved on one box.)
 constexpr int kSok = 1, kMov = 2;
-// Heterogeneous LDS tables: lds_mode 6 (a 4-bit station map, station coordinates | class, the
-// classes' rank indices -- half the bytes of mode 5's u16 cell entries) unless MEV_HET_U16
-#ifdef MEV_HET_U16
-constexpr bool kHetNib = false;
-#else
-constexpr bool kHetNib = true;
-#endif
 struct Ctx2 {
   int t, drawn, fl;
   int2 pos, wp;
@@ -1742,7 +1740,7 @@ struct Ctx2 {
 
 // FULL: every env of both groups exists (all pairs but the batch's last partial one): the
 // env / valid lane masks are constants, no per-step mask arithmetic.
-// HET: heterogeneous entities with a shared layout (KParams::lds_mode 5, build_het_lds): the
+// HET: heterogeneous entities with a shared layout (KParams::lds_mode 6, build_het_lds): the
 // lane's UE class hcu and movement parameters hmv (per UE, tb.mv); the association from the
 // LDS cell map of the closest station within any pair's reach, s*, which serves the UE when the
 // (class of s*, UE class) pair connects at that distance -- the closest station overall is then
@@ -1965,7 +1963,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
       full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) + 8u * k);
       cell[r] = ent[r] = 0;
     }
-  } else if (HET && kHetNib) {
+  } else if (HET) {
     // mode 6: s* per cell (4 bits, 15: none within reach), its coordinates and class, d2 to it,
     // the rank k of d2 in D of its class (the class's rank index); per (UE class, station) the
     // pair's {rate offset, largest connectable rank} (read beside the coordinates)
@@ -2004,37 +2002,6 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
         wait_vmem();
       }
       ent[r] = 0;
-    }
-  } else if (HET) {
-    // {s*, rank k of d2 in D of s*'s class} per cell; per (UE class, station): {the offset of
-    // the pair's rates over that D, the pair's largest connectable rank}
-    const int cells = KPS(W) * KPS(H);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      cell[r] = min(__umul24((uint32_t)c[r].pos.y, (uint32_t)KPS(W)) + (uint32_t)c[r].pos.x,
-                    (uint32_t)(cells - 1));
-      ent[r] = *reinterpret_cast<const uint16_t*>(lblob + 2u * cell[r]);
-      const bool has = ent[r] < 0xF000u;
-      const uint32_t s = has ? ent[r] >> 12 : 0u, k = has ? ent[r] & 4095u : 0u;
-      const int2 pk = *reinterpret_cast<const int2*>(lblob + kp.lds_st_off +
-                                                     8u * ((hpk & 15u) * (uint32_t)B + s));
-      const bool conn = has && (int)k <= pk.y;
-      full[r] = *reinterpret_cast<const double*>(lblob + KPS(lds_rate_off) +
-                                                 8u * (conn ? (uint32_t)pk.x + k : 0u));
-      srv[r] = active[r] && conn ? (int)s : -1;
-      // s* out of this class's reach (another station may serve it), or a rank past the
-      // table: the class's L2 map (rare, uniform branch; its load waited for inside)
-      const bool fb = active[r] && ((has && !conn) || ent[r] == 0xFFFFu);
-      if (bal(fb) & act_w[r]) {
-        if (fb) {
-          const int4 q = at(const_cast<int4*>(tb.assoc),
-                            16u * ((hpk & 15u) * (uint32_t)cells + cell[r]));
-          srv[r] = q.x;
-          full[r] = __hiloint2double(q.w, q.z);
-        }
-        wait_vmem();
-      }
-      ent[r] = 0;  // (the far-cell path below is this one's)
     }
   } else {
 #pragma unroll
@@ -2126,11 +2093,7 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // (reward_risky, rare: the exact reward's float32 bits instead, flag 0x100; the constants
     // from the blob's RewardC)
     const char* rcp = lblob + KPS(lds_r100_off) + 8 * kRewardCSlot;
-#ifdef MEV_NO_STEP_GUARD  // (dev A/B only: the two-group step without the guard)
-    const bool risky = false;
-#else
     const bool risky = lead && nact > 0 && (uint32_t)abs(isum) <= (uint32_t)nact * (uint32_t)kp.r_thr25;
-#endif
     int word0 = isum, flag = 0;
     if (bal(risky)) {
       // (every load landed before the call: the next pair's prefetch registers are not tracked
@@ -2442,8 +2405,7 @@ MEV_GUARD_FN void flush_fix(const int* srow, const float* obs_f, float* rew, con
     const int2 v = *reinterpret_cast<const int2*>(srow + 2 * q);
     const uint32_t b = (uint32_t)v.y;
     const int nact = (int)(b & 0x7fu);
-    if ((b & 0x100u) || !(nact > 0 && fabsf((float)v.x * 0x1p-25f) * 9.5e-6f <=
-                                          (float)nact * (c.u_err + 0x1p-25f)))
+    if ((b & 0x100u) || !(nact > 0 && (uint32_t)abs(v.x) <= (uint32_t)nact * (uint32_t)c.thr25))
       continue;
     const float* rates = obs_f + 4 * ((size_t)(row0 + r) * (size_t)E + (size_t)(e0 + j)) * (size_t)U + 2;
     long long su = 0;
@@ -2467,9 +2429,9 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
   lds_barrier();
   const float inv_nwg = 1.0f / (float)NWG;
   bool any = false;
-  // (the test in float32 against u_err: 92.5 vs 95.5 us per 200-step launch at 4,096 medium envs
-  // for the integer form against r_thr25, interleaved on one box)
-  const float u_err = DETECT ? *reinterpret_cast<const float*>(rc + 24) : 0.f;
+  // (the same test as the two-group and packed steps' in-step one -- the integer compare of the
+  // 2^-25 sum against nact r_thr25 -- so every kernel shape sends the same rows to the exact path)
+  const uint32_t thr25 = DETECT ? *reinterpret_cast<const uint32_t*>(rc + 28) : 0u;
   for (int q = threadIdx.x; q < nr * NWG; q += (int)blockDim.x) {
     // q / NWG through float (q + 1/2 is >= 1/2 away from a multiple of NWG; exact for q < 2^22)
     const int r = (int)(((float)q + 0.5f) * inv_nwg), j = q - r * NWG;
@@ -2485,8 +2447,7 @@ __device__ __forceinline__ void flush_staged2(const KOut& out, const int* srow, 
                        : nact > 0 ? (float)v.x * 0x1p-25f * __builtin_amdgcn_rcpf((float)nact) : lower;
       at(out.done + ro, o) = (uint8_t)((b >> 7) & 1u);
       if (DETECT)
-        any = any || (!(b & 0x100u) && nact > 0 &&
-                      fabsf((float)v.x * 0x1p-25f) * 9.5e-6f <= (float)nact * (u_err + 0x1p-25f));
+        any = any || (!(b & 0x100u) && nact > 0 && (uint32_t)abs(v.x) <= (uint32_t)nact * thr25);
     }
   }
   if (DETECT && __syncthreads_or(any)) {  // rare
@@ -2883,12 +2844,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         }
         emit(sn, pipe_emit_front<UC, SCN>(kp, m, sn, pipe_cell<UC, SCN>(kp, sn, lblob), lblob, hist));
       } else {
-#ifdef MEV_LDS2_FULL
-        if (nok[R - 1] == G) steps(std::true_type{});
-        else steps(std::false_type{});
-#else
         steps(std::false_type{});
-#endif
       }
       MEV_TS(min(3 + 3 * it, 27));
       // the state after the last step (see k_steps_packed), as unconditional buffer stores; the
@@ -4018,15 +3974,15 @@ __global__ void k_lds_map3(const int4* __restrict__ map, int cells, const uint2*
   }
 }
 
-// Heterogeneous entities with a shared layout, LDS form (KParams::lds_mode 5, the two-group
+// Heterogeneous entities with a shared layout, LDS form (KParams::lds_mode 6, the two-group
 // rollout's HET instances), built per layout on the device:
 //   k_het_cells: per cell the closest station s* within `reach` (the largest pair d2max; ties to
 //     the lower index) and its squared distance, flagged in the set D_cb of its station class cb;
 //   k_d2_prefix (per class): the rank index of each D_cb;
 //   k_het_info: T = sum |D_cb|, the class bases, and per (UE class cu, station j) the pair's
 //     rate offset cu T + base_cb(j) and its largest connectable rank (d2 <= the pair's d2max);
-//   k_het_map: the u16 cell entries (s* << 12 | rank of d2 in D_cb; 0xF000 nothing in reach,
-//     0xFFFF rank past 4,094) and the rates [cu][cb][k] of every pair over D_cb.
+//   k_het_map: the 4-bit s* per cell (15: nothing in reach) and the rates [cu][cb][k] of every
+//     pair over D_cb.
 __global__ void k_het_cells(const int2* __restrict__ bs, int B, int W, int H, int reach,
                             const uint8_t* __restrict__ bs_cls, int2* __restrict__ cellv,
                             uint8_t* __restrict__ flag) {
@@ -4094,9 +4050,9 @@ __global__ void k_het_map(const int2* __restrict__ cellv, int cells, const uint2
                           int nwords, int reach, int NB, int NU, const uint8_t* __restrict__ bs_cls,
                           const int2* __restrict__ pair, const double* __restrict__ rate_full,
                           const int* __restrict__ info, uint8_t* __restrict__ blob, int rate_off,
-                          int rate_cap, int nib) {
+                          int rate_cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (nib && 2 * i < cells) {  // (mode 6) s* per cell, 4 bits, two cells a byte
+  if (2 * i < cells) {  // s* per cell, 4 bits, two cells a byte
     uint32_t v = 0;
     for (int h = 0; h < 2; ++h) {
       const int cl = 2 * i + h;
@@ -4104,16 +4060,6 @@ __global__ void k_het_map(const int2* __restrict__ cellv, int cells, const uint2
       v |= (uint32_t)(sx < 0 ? 15 : sx) << (4 * h);
     }
     blob[i] = (uint8_t)v;
-  }
-  if (!nib && i < cells) {
-    const int2 v = cellv[i];
-    uint32_t ent = 0xF000u;  // nothing within any pair's reach
-    if (v.x >= 0) {
-      const uint32_t k = het_rank(words + (size_t)bs_cls[v.x] * (nwords + 1), nwords, (uint32_t)v.y,
-                                  (uint32_t)reach);
-      ent = k < kLds3Rates - 1 ? ((uint32_t)v.x << 12) | k : 0xFFFFu;
-    }
-    reinterpret_cast<uint16_t*>(blob)[i] = (uint16_t)ent;
   }
   const int nd = reach + 1;
   if (i < NB * nd) {
@@ -4244,9 +4190,11 @@ struct mev_ctx {
   uint8_t* h_ucl;
   int2* h_pair;
   MoveP* h_mv;
+  int het_snap_wide;  // some UE's d2snap needs more than 24 bits (velocity >= 4,096): no mode-6
+                      // LDS tables (their per-lane word packs d2snap << 8)
   int16_t* h_perm;
   int* h_seg;
-  // heterogeneous entities on the two-group rollout: KParams::lds_mode 5 tables of the shared
+  // heterogeneous entities on the two-group rollout: KParams::lds_mode 6 tables of the shared
   // layout (mev_update_stations: k_het_cells / k_d2_prefix / k_het_info / k_het_map; their
   // rate count read back like mode 3's |D|, through dcount_pin); het_lds 0: packed kernels only
   int het_lds;
@@ -4276,6 +4224,11 @@ static thread_local char g_hip_err[256] = "";
 // Exported functions get C linkage from their declarations in mev.h.
 
 int mev_abi_version(void) { return MEV_ABI_VERSION; }
+
+#ifndef MEV_SRC_HASH
+#define MEV_SRC_HASH "unknown"
+#endif
+const char* mev_source_hash(void) { return MEV_SRC_HASH; }
 
 const char* mev_last_hip_error(void) { return g_hip_err; }
 
@@ -4725,6 +4678,8 @@ static int build_het(mev_ctx* c) {
   }
   std::vector<MoveP> mv(U);
   for (int u = 0; u < U; ++u) mv[u] = host_move_params(vel[u], p->width, p->height, all15);
+  c->het_snap_wide = 0;
+  for (int u = 0; u < U; ++u) c->het_snap_wide |= mv[u].d2snap >= (1 << 24) ? 1 : 0;
   // stations grouped by class, each segment padded to an even length (pairs of keys)
   std::vector<int16_t> perm;
   std::vector<int> seg(NB + 1, 0);
@@ -4759,31 +4714,29 @@ static int build_het(mev_ctx* c) {
   return MEV_OK;
 }
 
-// The two-group rollout's tables for heterogeneous entities with a shared layout (lds_mode 5),
-// allocated here and filled per layout by mev_update_stations. Blob: [0, 2 cells) the u16 cell
-// entries, [r100_off, +576) 100 / n, [st_off, +8 NU B) the {offset, largest rank} of each (UE
-// class, station) pair, [rate_off, ...) the pairs' runs of rates. Eligible: U = 15 / 30, at most
-// 15 stations (4-bit station field), a draw table, cells < 65,536 rounded into LDS beside at least
-// one wavefront; two_groups >= 0 and lds_tables >= 0.
+// The two-group rollout's tables for heterogeneous entities with a shared layout (lds_mode 6),
+// allocated here and filled per layout by mev_update_stations (blob layout below). Eligible:
+// U = 15 / 30, at most 15 stations (4-bit station field), a draw table, cells < 65,536 rounded
+// into LDS beside at least one wavefront, every UE's d2snap within 24 bits; two_groups >= 0 and
+// lds_tables >= 0.
 static int build_het_lds(mev_ctx* c) {
   const KParams& kp = c->kp;
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   c->het_lds = 0;
   const size_t cells = (size_t)c->p.width * c->p.height;
   if (!c->het_packed || c->p.two_groups < 0 || c->p.lds_tables < 0 || !(kp.U == 15 || kp.U == 30) ||
-      kp.B > 15 || kp.tab_m <= 0 || cells >= 65536 || c->d2max < 0 ||
-      (kHetNib && (c->p.width > 4096 || c->p.height > 4096)))
+      kp.B > 15 || kp.tab_m <= 0 || cells >= 65536 || c->d2max < 0 || c->het_snap_wide ||
+      c->p.width > 4096 || c->p.height > 4096)
     return MEV_OK;
   const int NB = kp.nb_cls, NU = kp.nu_cls;
   const size_t nwords = (size_t)c->d2max / 32 + 1;
   // mode 6: [0, nib) 4-bit s* per cell; [st, +64) station x | y << 12 | class << 24; [pk,
   // +8 NU B) pairs; [words, +8 NB (nwords + 1)) the classes' rank indices; [r100, +576); rates.
-  // mode 5: [0, 2 cells) u16 entries; [r100, +576); [pk = st_off, +8 NU B); rates.
   const size_t nib_bytes = up16((cells + 1) / 2);
   const size_t pk6 = nib_bytes + 64, words6 = up16(pk6 + 8 * (size_t)NU * kp.B);
-  const size_t r100_off = kHetNib ? up16(words6 + 8 * (size_t)NB * (nwords + 1)) : up16(2 * cells);
-  const size_t st_off = kHetNib ? pk6 : r100_off + 8 * 72;  // (the pairs' table)
-  const size_t rate_off = kHetNib ? up16(r100_off + 8 * 72) : up16(st_off + 8 * (size_t)NU * kp.B);
+  const size_t r100_off = up16(words6 + 8 * (size_t)NB * (nwords + 1));
+  const size_t st_off = pk6;  // (the pairs' table)
+  const size_t rate_off = up16(r100_off + 8 * 72);
   const size_t one_wave = lds2_per_wave(kp.envs_per_wave, kp.B, kp.tab_m, 1) +
                           (size_t)2 * kp.envs_per_wave * kStage2Bytes + 4;
   if (rate_off + one_wave + 8 * 64 > (size_t)kLds2BytesPerWG) return MEV_OK;
@@ -4798,8 +4751,7 @@ static int build_het_lds(mev_ctx* c) {
       hipMalloc(&c->het_blob, rate_off + 8 * (size_t)cap) != hipSuccess)
     return MEV_ENOMEM;
   MEV_HIP(hipMemset(c->het_blob, 0, rate_off + 8 * (size_t)cap));
-  if (kHetNib) MEV_HIP(hipMemset(c->het_blob, 0xff, (cells + 1) / 2));  // no station until a layout
-  else MEV_HIP(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(c->het_blob), 0xF000, cells));
+  MEV_HIP(hipMemset(c->het_blob, 0xff, (cells + 1) / 2));  // no station until a layout
   double r100[72] = {0.0};
   for (int n = 1; n <= 64; ++n) r100[n] = 100.0 / (double)n;  // correctly rounded (IEEE host)
   MEV_HIP(hipMemcpy(c->het_blob + r100_off, r100, sizeof(r100), hipMemcpyHostToDevice));
@@ -4897,6 +4849,10 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
   kp.u_upperf = (float)kp.upper;
   kp.u_scale = (float)(2.0 / (kp.upper - kp.lower));
   kp.u_offset = (float)(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
+  // with offset 0 and w2 0 the float32 utility is ur * scale with ur = c log2(r): its relative
+  // error is that of log2 at r = cents / 100 != 1 (|log2 r| >= log2 1.01), within 1e-5; otherwise
+  // the sum cancels near the utility's zero and only an absolute bound holds (utility_f32r)
+  kp.util_exact = (kp.u_offset != 0.f || kp.u_w2f != 0.f) ? 1 : 0;
   kp.xcd_remap = params->xcd_remap < 0 ? 0 : params->xcd_remap > 1 ? 1 + (params->xcd_remap - 1) % 8 : 1;
   kp.st8 = params->compact_state;
   if (params->num_ues > 64 && params->station_culling >= 0) {  // block kernel (block_cull_params)
@@ -4938,6 +4894,8 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
       kp.u_err = (float)(2.0 * (A * ((3.0 * 0x1p-24 + 2.2e-8) / log(2.0) + 0x1p-22 * lmax) +
                                0x1p-22 * (1.0 + off + sc)));
       if (params->reward_exact > 0) kp.u_err = INFINITY;  // (every row takes the exact path)
+      // (tests: a band -reward_exact times wider, so that a subset of rows takes the exact path)
+      if (params->reward_exact < -1) kp.u_err *= (float)-params->reward_exact;
       // |sum| 9.5e-6 <= nact (u_err + q) as bounds on the mean (q = 2^-24, the coarser fixed
       // point; 0.1 % wider): |mean| <= r_thr, and on the 2^-25 sum |isum| <= nact r_thr25, unsigned
       // (every |isum| <= nact 2^25 <= 2^31: the caps take every row in reward_exact)
@@ -5048,7 +5006,7 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     rc = build_het_lds(c);
     if (rc) return rc;
   }
-  if ((c->blob && c->kp.lds_mode == 3) || c->het_lds) {  // |D| (mode 3) / the rate count (mode 5)
+  if ((c->blob && c->kp.lds_mode == 3) || c->het_lds) {  // |D| (mode 3) / the rate count (mode 6)
                                                        // of each layout, read back without a sync
     MEV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->dcount_pin), sizeof(int), hipHostMallocDefault));
     MEV_HIP(hipEventCreateWithFlags(&c->ev_dcount, hipEventDisableTiming));
@@ -5174,7 +5132,7 @@ int mev_last_launch_kind(const mev_ctx* c) { return c ? c->last_kind : MEV_EINVA
 
 int mev_rollout_instance(const mev_ctx* c) {
   if (!c) return MEV_EINVAL;
-  const bool lean_ok = !c->kp.util_direct;
+  const bool lean_ok = !c->kp.util_direct && !c->kp.util_exact;
   return (lean_ok && ((c->kp.lds_assoc > 0 && ((c->kp.lds_mode == 3 && !c->p.bs_per_env) ||
                                                 (c->kp.lds_mode == 4 && c->p.bs_per_env))) ||
                       (c->kp.U > 64 && c->p.bs_per_env && !c->kp.het)))
@@ -5298,7 +5256,8 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                                const LaunchEv& ev) {
   const KParams& kp = c->kp;
   const int groups = (kp.E + kp.envs_per_wave - 1) / kp.envs_per_wave;
-  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
+  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct &&
+                    !kp.util_exact;
   StepKernel k = step_kernel_for(c->p.bs_per_env != 0, lean, kp.U);
   // scenario constants; tie-free share with the blob's 100 / n table (k_step_packed TF)
   const bool tf1 = c->tie_free && c->blob != nullptr;
@@ -5341,16 +5300,16 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
       c->last_kind = MEV_KIND_LDS2_PERENV;
       return MEV_OK;
     }
-    // heterogeneous entities with a shared layout: k_steps_lds2 HET on the lds_mode 5 tables
+    // heterogeneous entities with a shared layout: k_steps_lds2 HET on the lds_mode 6 tables
     // (build_het_lds) when the layout's rates fit beside at least one wavefront
     if (c->het_lds && lean && traj && pre_ok && c->p.two_groups >= 0 && c->p.two_groups <= 2) {
       const int nrate = layout_dcount(c);
       if (nrate >= 0 && nrate <= c->het_rate_cap) {
         // mode 6 (the 4-bit station map: 92 KB of tables on the large layout): two groups per
         // wavefront unless two_groups = 2 -- at 65,536 mobile-large-mixed envs 2.93 vs 3.29 ms
-        // per 200-step launch; mode 5 (u16 entries, 136 KB: ~10 two-group waves per workgroup):
-        // one group unless two_groups = 1 -- 2.93 vs 4.05 ms (interleaved on one box)
-        const int R = c->p.two_groups == 1 ? 2 : c->p.two_groups == 2 ? 1 : kHetNib ? 2 : 1;
+        // per 200-step launch (the dropped mode 5, u16 cell entries of 136 KB: ~10 two-group
+        // waves per workgroup, 2.93 with one group vs 4.05 ms with two; interleaved on one box)
+        const int R = c->p.two_groups == 2 ? 1 : 2;
         const int G = kp.envs_per_wave;
         const int units = R == 2 ? pairs : groups;
         const size_t blob = ((size_t)c->het_rate_off + 8 * (size_t)nrate + 15) & ~(size_t)15;
@@ -5384,9 +5343,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
           }
           const int blocks = std::min((units + nw2 - 1) / nw2, c->het_cus * c->het_occ_n);
           KParams kp5 = kp;
-          kp5.lds_mode = kHetNib ? 6 : 5;
+          kp5.lds_mode = 6;
           kp5.lds_assoc = (int)blob;
-          kp5.lds_st_off = kHetNib ? c->het_nib_st : c->het_st_off;
+          kp5.lds_st_off = c->het_nib_st;
           kp5.lds_r16_off = c->het_st_off;     // (mode 6: the pairs' table)
           kp5.lds_rank_off = c->het_words_off;  // (mode 6)
           kp5.lds_rate_off = c->het_rate_off;
@@ -5561,7 +5520,8 @@ static int launch_block_steps(const mev_ctx* c, const KState& ks, const KOut& ko
                               const LaunchEv& ev) {
   const KParams& kp = c->kp;
   if (nsteps <= 0) return MEV_OK;
-  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct;
+  const bool lean = !ko.rate64 && !ko.util64 && !ko.metrics && !ko.qoe_stats && !kp.util_direct &&
+                    !kp.util_exact;
   const bool per_env = c->p.bs_per_env != 0;
   void (*kf)(KParams, KState, KOut, KTables, int, int) =
       kp.het ? (per_env ? (lean ? k_steps_block<true, true, true> : k_steps_block<true, false, true>)
@@ -5645,7 +5605,7 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                        reinterpret_cast<const int2*>(bs_xy), c->p.num_bs, c->p.width,
                        c->p.height, c->h_bcl, c->h_pair, c->kp.nu_cls, c->rate_full, c->assoc);
     MEV_HIP(hipGetLastError());
-    if (c->het_lds) {  // the two-group rollout's tables (lds_mode 5), see build_het_lds
+    if (c->het_lds) {  // the two-group rollout's tables (lds_mode 6), see build_het_lds
       const int NB = c->kp.nb_cls, NU = c->kp.nu_cls, reach = c->het_reach, nw = c->het_nwords;
       const int nd = reach + 1;
       hipStream_t s = (hipStream_t)stream;
@@ -5660,14 +5620,14 @@ int mev_update_stations(const mev_ctx* c, const int32_t* bs_xy, void* stream) {
                          c->p.num_bs, c->h_bcl, c->h_pair, reach,
                          reinterpret_cast<int2*>(c->het_blob + c->het_st_off), c->het_info,
                          reinterpret_cast<const int2*>(bs_xy),
-                         kHetNib ? reinterpret_cast<uint32_t*>(c->het_blob + c->het_nib_st) : nullptr);
+                         reinterpret_cast<uint32_t*>(c->het_blob + c->het_nib_st));
       const int n = std::max(cells, NB * nd);
       hipLaunchKernelGGL(k_het_map, dim3((n + 255) / 256), dim3(256), 0, s, c->het_cell, cells,
                          c->het_words, nw, reach, NB, NU, c->h_bcl, c->h_pair, c->rate_full,
-                         c->het_info, c->het_blob, c->het_rate_off, c->het_rate_cap, kHetNib ? 1 : 0);
+                         c->het_info, c->het_blob, c->het_rate_off, c->het_rate_cap);
       MEV_HIP(hipGetLastError());
-      if (kHetNib)  // the classes' rank indices into the blob
-        MEV_HIP(hipMemcpyAsync(c->het_blob + c->het_words_off, c->het_words,
+      // the classes' rank indices into the blob
+      MEV_HIP(hipMemcpyAsync(c->het_blob + c->het_words_off, c->het_words,
                                sizeof(uint2) * (size_t)NB * (nw + 1), hipMemcpyDeviceToDevice, s));
       MEV_HIP(hipMemcpyAsync(c->dcount_pin, c->het_info, sizeof(int), hipMemcpyDeviceToHost, s));
       MEV_HIP(hipEventRecord(c->ev_dcount, s));

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "MEV_LIB", os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmev.so")))
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 MEV_OK = 0
 MEV_EINVAL = -22
 MEV_ENOMEM = -12
@@ -22,7 +22,7 @@ MEV_EHIP = -1000
 MEV_ECHANNEL = -1001
 
 # every symbol include/mev.h declares (tests check the library exports all of them)
-EXPORTS = ("mev_abi_version", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes", "mev_state_bytes_per_ue",
+EXPORTS = ("mev_abi_version", "mev_source_hash", "mev_create", "mev_destroy", "mev_d2max", "mev_launch_parts", "mev_step_shape", "mev_lds_tables_bytes", "mev_state_bytes_per_ue",
            "mev_rate_table", "mev_copy_rate_table", "mev_seed_pcg64", "mev_seed_pcg64_device",
            "mev_update_stations", "mev_update_layouts", "mev_build_rate_table", "mev_share_cents",
            "mev_rollout_instance", "mev_share_tie_free", "mev_last_launch_kind",
@@ -79,6 +79,22 @@ class MevError(RuntimeError):
 
 _LIB = None
 _LOCK = threading.Lock()
+SOURCES = (os.path.normpath(os.path.join(_HERE, "..", "..", "csrc", "mev_step.hip")),
+           os.path.normpath(os.path.join(_HERE, "..", "..", "..", "include", "mev.h")))
+
+
+def source_hash():
+    """First 16 hex digits of SHA-256(mev_step.hip + mev.h) -- the Makefile's MEV_SRC_HASH --
+    or None when the sources are not beside the library (an installed copy)."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in SOURCES:
+        try:
+            with open(path, "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return None
+    return h.hexdigest()[:16]
 
 
 def lib():
@@ -155,6 +171,13 @@ def lib():
         L.mev_last_hip_error.restype = C.c_char_p
         if L.mev_abi_version() != ABI_VERSION:
             raise ImportError(f"libmev ABI {L.mev_abi_version()} != expected {ABI_VERSION}")
+        L.mev_source_hash.restype = C.c_char_p
+        built, src = L.mev_source_hash().decode(), source_hash()
+        if src is not None and built != src and not os.environ.get("MEV_LIB"):
+            raise ImportError(
+                f"stale libmev.so at {LIB_PATH}: compiled from sources {built}, the sources next "
+                f"to it hash to {src} -- rebuild with `make -C mobile-env-gan_amd/csrc` or "
+                "__graft_entry__.build()")
         _LIB = L
         return L
 

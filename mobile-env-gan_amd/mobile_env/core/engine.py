@@ -361,7 +361,9 @@ class StepEngine:
     @property
     def rollout_instance(self) -> int:
         """Rollout kernel instance: 0 generic, s > 0 registered scenario s with constants."""
-        return int(self._lib.mev_rollout_instance(self._ctx))
+        code = int(self._lib.mev_rollout_instance(self._ctx))
+        N.check(min(code, 0), "mev_rollout_instance")  # (negative: a null or closed context)
+        return code
 
     #: mev_last_launch_kind codes (include/mev.h MEV_KIND_*)
     LAUNCH_KINDS = {0: None, 1: "packed_step", 2: "packed_fused", 3: "lds2_two_groups",
@@ -372,7 +374,12 @@ class StepEngine:
     def last_launch_kind(self) -> "str | None":
         """The step kernel the last step() / rollout() launched (mev_last_launch_kind): every
         kind computes the same results; tests use it to pin which kernel they checked."""
-        return self.LAUNCH_KINDS[int(self._lib.mev_last_launch_kind(self._ctx))]
+        code = int(self._lib.mev_last_launch_kind(self._ctx))
+        if code < 0:  # MEV_EINVAL: a null or closed context
+            N.check(code, "mev_last_launch_kind")
+        if code not in self.LAUNCH_KINDS:
+            raise N.MevError(N.MEV_EINVAL, f"mev_last_launch_kind: unknown kind {code}")
+        return self.LAUNCH_KINDS[code]
 
     @property
     def share_tie_free(self) -> bool:

@@ -95,10 +95,10 @@ def test_make_reset_step_matches_oracle(env_id):
         np.testing.assert_allclose(o4[..., 2], o["rate"].astype(np.float32), rtol=1e-5)
         if sp["mode"] == "central":
             np.testing.assert_allclose(rew.cpu().numpy(), o["metrics"][:, 2], rtol=1e-5,
-                                       atol=1e-7)
+                                       atol=0)
         else:
             np.testing.assert_allclose(rew.cpu().numpy(), o["util"].astype(np.float32),
-                                       rtol=1e-5, atol=1e-7)
+                                       rtol=1e-5, atol=0)
         np.testing.assert_array_equal(trunc.cpu().numpy(), o["done"])
         assert not term.any()
     env.close()
@@ -142,7 +142,7 @@ def test_make_custom_layouts_are_the_fixture_layouts():
         o4 = obs.cpu().numpy().reshape(E, 1024, 4)
         np.testing.assert_allclose(o4[..., 2], d["rate"][:, s].astype(np.float32), rtol=1e-5)
         np.testing.assert_allclose(rew.cpu().numpy(), d["metrics"][:, s, 2], rtol=1e-5,
-                                   atol=1e-7)
+                                   atol=0)
     env.close()
 
 

@@ -35,9 +35,9 @@ def _check_host(d, name, s, idx, obs, srv, rew, done, rate64=None, util64=None, 
                                err_msg=tag + " rate")
     ru = d["util"][idx, s]
     act = ~np.isnan(ru)
-    np.testing.assert_allclose(obs[..., 3][act], ru[act].astype(np.float32), rtol=RTOL, atol=1e-7,
+    np.testing.assert_allclose(obs[..., 3][act], ru[act].astype(np.float32), rtol=RTOL, atol=0,
                                err_msg=tag + " utility")
-    np.testing.assert_allclose(rew, d["metrics"][idx, s, 2], rtol=RTOL, atol=1e-7,
+    np.testing.assert_allclose(rew, d["metrics"][idx, s, 2], rtol=RTOL, atol=0,
                                err_msg=tag + " reward")
     np.testing.assert_array_equal(done.astype(bool), np.full(len(done), knob_done(d)[s]),
                                   err_msg=tag + " done")
@@ -133,9 +133,9 @@ def test_knob_lean_rollout_at_scale(name):
         torch.testing.assert_close(tr.obs[s, ..., 2], rate, rtol=RTOL, atol=0)
         ru = torch.from_numpy(d["util"][:, s]).to(dev)[idx].float()
         act = ~torch.isnan(ru)
-        torch.testing.assert_close(tr.obs[s, ..., 3][act], ru[act], rtol=RTOL, atol=1e-7)
+        torch.testing.assert_close(tr.obs[s, ..., 3][act], ru[act], rtol=RTOL, atol=0)
         rew = torch.from_numpy(d["metrics"][:, s, 2]).to(dev)[idx].float()
-        torch.testing.assert_close(tr.reward[s], rew, rtol=RTOL, atol=1e-7)
+        torch.testing.assert_close(tr.reward[s], rew, rtol=RTOL, atol=0)
         assert bool((tr.done[s] == int(done[s])).all()), f"{name} step {s} done"
     final = [eng.ue_state.clone(), synced_pcg(eng).clone(), eng.t.clone()]
     eng.close()

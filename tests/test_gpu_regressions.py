@@ -114,9 +114,18 @@ def test_layout_change_then_pipelined_rollout_vs_oracle():
     new_bs = (np.asarray(L["bs"]) + 7) % 200
     eng.set_bs_layout(torch.as_tensor(new_bs, dtype=torch.int32))
     tr = eng.rollout(45)  # the next episodes: lazy reset, then the new layout throughout
-    assert eng.last_launch_kind in ("lds2_pipelined", "packed_fused")
+    assert eng.last_launch_kind == "lds2_pipelined"  # (|D| of the shifted layout <= 4,094)
     ob = OracleBatch(OracleParams(), new_bs.tolist(), U, seeds)
     assert_rollout_vs_oracle(tr, ob, 45)
+    # every station in the map's corner: the serving distances run over every sum of two squares
+    # within reach (|D| = 5,101 > 4,094, past the mode-3 ranks) -- the read-back |D| of THIS
+    # layout must reach the choice: not the pipelined kernel, and the oracle's results
+    far_bs = np.zeros((B, 2), dtype=np.int64)
+    eng.set_bs_layout(torch.as_tensor(far_bs, dtype=torch.int32))
+    tr = eng.rollout(25)  # (mid-episode: the new layout from the next step on, like the oracle's)
+    assert eng.last_launch_kind == "packed_fused"
+    ob.bs_xy[:] = far_bs  # (the same oracle envs continue on the new layout)
+    assert_rollout_vs_oracle(tr, ob, 25)
     eng.close()
 
 
@@ -217,3 +226,49 @@ def test_float32_utility_within_the_guards_bound(lower, upper, coeffs):
     eng.close()
     bound = _u_err(lower, upper, *coeffs)
     assert worst <= bound / 2, (worst, bound)
+
+
+@pytest.mark.parametrize("size,k", [("large", 5), ("medium", 3)])
+def test_reward_guard_partial_band_same_rows_every_shape(size, k):
+    """The reward guard decides which env-steps take the exact path with ONE test in every
+    kernel shape (the 2^-25 fixed-point sum against nact r_thr25): the two-group step's in-step
+    test, the pipelined loop's flush (DETECT), the packed kernels' leaders. With the band made k
+    times wider (reward_exact = -k: |mean| up to ~0.81 / ~0.49 instead of 0.166, which no
+    large / medium env-step reaches) a subset of the rows -- some, not all -- takes the exact
+    path; every shape then gives the same reward bits, the rows well inside the band are within
+    one float32 ulp of the oracle's float64 mean (the exact path), and every row within 1e-5
+    relative (atol 0) of it."""
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS[size]
+    U, B, E, n = L["num_ues"], len(L["bs"]), 2000, 25
+    seeds = 777 + 3 * np.arange(E)
+    got = {}
+    for tg, kind in ((3, "lds2_pipelined"), (1, "lds2_two_groups"), (-1, "packed_fused")):
+        eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B, two_groups=tg,
+                                      reward_exact=-k), L["bs"], seeds, device="cuda")
+        tr = eng.rollout(n)
+        assert eng.last_launch_kind == kind
+        got[kind] = tr.reward.cpu().numpy()
+        eng.close()
+    eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B, reward_exact=-k), L["bs"],
+                     seeds, device="cuda")
+    rows = []
+    for _ in range(n):
+        eng.step()
+        rows.append(eng.reward.cpu().numpy())
+    assert eng.last_launch_kind == "packed_step"
+    got["packed_step"] = np.stack(rows)
+    eng.close()
+    ref = got["lds2_pipelined"]
+    for k, v in got.items():
+        np.testing.assert_array_equal(v, ref, err_msg=f"{k} vs lds2_pipelined")
+    ob = OracleBatch(OracleParams(), L["bs"], U, seeds)
+    want = np.stack([ob.step()["metrics"][:, 2] for _ in range(n)])
+    np.testing.assert_allclose(ref, want, rtol=1e-5, atol=0)
+    # the band on the mean (mev_create: |isum| <= nact r_thr25, r_thr25 from k u_err)
+    thr = (k * _u_err(-20.0, 20.0, 10.0, 0.0, 10.0) + 2.0 ** -24) / 9.5e-6 * 1.001
+    inside, outside = np.abs(want) < 0.9 * thr, np.abs(want) > 1.1 * thr
+    assert inside.mean() > 0.005 and outside.mean() > 0.005, (thr, inside.mean(), outside.mean())
+    np.testing.assert_allclose(ref[inside], want[inside].astype(np.float32), rtol=1.2e-7, atol=0)

@@ -16,10 +16,15 @@ every step's outputs with the oracle (oracle/vec.py, pinned to the reference's f
   -- envs are independent, so the subset comparison is exact;
 * the Gym step() launch of both (mev_step(1), one launch per step);
 * the build-defined mobile-large-mixed-v0 (heterogeneous classes) at 65,536 envs -> the
-  two-group kernel on the lds_mode 5 tables, every 16th env against the oracle.
+  two-group kernel on the lds_mode 6 tables, every 16th env against the oracle;
+* BASELINE configs[4]: mobile-custom-128x1024-v0 at 1,024 envs (its per-GPU batch of 8,192 over
+  8 GPUs) -> the lean scenario-constant block kernel (k_steps_block, instance 4: f32 utility,
+  fixed-point reward, station-culling records built in LDS), every 16th env against the oracle
+  on that env's own 128-station layout; and its Gym step() launch (the two-UEs-per-lane block
+  instance with the HBM culling records).
 
 Bars (north_star): positions, serving, done bit-exact; float32 rate / utility / reward within
-1e-5 relative (rewards of magnitude >= 1e-3 with atol 0, helpers.assert_step_vs_oracle).
+1e-5 relative with atol 0 (helpers.assert_step_vs_oracle).
 Reference: base.py:230-296 (step), movement.py:42-62 (RandomWaypoint), channels.py:133-146.
 """
 import numpy as np
@@ -129,3 +134,59 @@ def test_mixed_65536_rollout_strided_vs_oracle():
     del tr
     env.close()
     torch.cuda.empty_cache()
+
+
+def _custom_oracle(env, idx):
+    from mobile_env.scenarios.registry import spec
+    from oracle.vec import OracleBatch, OracleParams
+    vel = float(spec("mobile-custom-128x1024-v0")["velocity"])
+    bs = env.engine.bs_xy.cpu().numpy()[idx]  # [E', 128, 2]: each env's own layout
+    cnt = env.engine.bs_count.cpu().numpy()[idx] if env.engine.bs_count is not None else None
+    return OracleBatch(OracleParams(velocity=vel), bs, env.num_ues, env.seeds.numpy()[idx],
+                       bs_count=cnt)
+
+
+def test_custom_1024_shipped_rollout_vs_oracle():
+    """BASELINE configs[4] (128 BS x 1,024 UE, velocity 10, per-env layouts drawn from each env's
+    seed) at 1,024 envs with make()'s own choice -- the lean scenario-constant block rollout: one
+    45-step launch (two episode resets; station culling active, >= 32 steps), every 16th env
+    against the oracle step by step, then the final positions."""
+    import mobile_env
+    import torch
+    E, n, stride = 1024, 45, 16
+    env = mobile_env.make("mobile-custom-128x1024-v0", num_envs=E, device="cuda:0", seed=600)
+    env.reset()
+    eng = env.engine
+    assert eng.rollout_instance == 4 and eng.bs_per_env
+    tr = eng.rollout(n)
+    assert eng.last_launch_kind == "block"
+    idx = np.arange(0, E, stride)
+    o = assert_rollout_vs_oracle(tr, _custom_oracle(env, idx), n, env_idx=idx)
+    ti = torch.as_tensor(idx, device=eng.device)
+    np.testing.assert_array_equal(eng.ue_xy.index_select(0, ti).cpu().numpy(), o["xy"])
+    del tr
+    env.close()
+    torch.cuda.empty_cache()
+
+
+def test_custom_1024_gym_step_vs_oracle():
+    """The Gym surface of BASELINE configs[4] at 1,024 envs: 22 one-step launches (the reset
+    inside), every 16th env against the oracle each step."""
+    import mobile_env
+    import torch
+    E, stride = 1024, 16
+    env = mobile_env.make("mobile-custom-128x1024-v0", num_envs=E, device="cuda:0", seed=700)
+    env.reset()
+    idx = np.arange(0, E, stride)
+    ti = torch.as_tensor(idx, device=env.device)
+    ob = _custom_oracle(env, idx)
+    U = env.num_ues
+    for s in range(22):
+        obs, reward, term, trunc, info = env.step()
+        assert env.engine.last_launch_kind == "block"
+        o = ob.step()
+        obs = obs.view(E, U, 4).index_select(0, ti).cpu().numpy()
+        assert_step_vs_oracle(o, obs, info["serving"].index_select(0, ti).cpu().numpy(),
+                              reward.index_select(0, ti).cpu().numpy(),
+                              trunc.index_select(0, ti).cpu().numpy(), where=f"step {s}")
+    env.close()

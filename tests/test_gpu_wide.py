@@ -28,7 +28,7 @@ def _check_row(d, s, xy, srv, rate, util, reward):
     np.testing.assert_array_equal(rate, d["rate"][:, s], err_msg=f"rates step {s}")
     act = ~np.isnan(d["util"][:, s])
     np.testing.assert_allclose(util[act], d["util"][:, s][act], rtol=1e-12, atol=0)
-    np.testing.assert_allclose(reward, d["metrics"][:, s, 2], rtol=RTOL, atol=1e-7)
+    np.testing.assert_allclose(reward, d["metrics"][:, s, 2], rtol=RTOL, atol=0)
 
 
 @pytest.mark.parametrize("name", WIDE_FIXTURES)

@@ -27,6 +27,8 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     assert sorted(N.EXPORTS) == syms
     assert lib.mev_abi_version() == N.ABI_VERSION
+    # build provenance: the library was compiled from the sources beside it
+    assert lib.mev_source_hash().decode() == N.source_hash() != "unknown"
 
 
 def test_struct_layout_matches_header():
@@ -390,6 +392,12 @@ def test_prefetch_registers_check_on_generated_assembly():
     assert cp.violations(call)[0]
     waited = call.replace("; %bb.1:\n", "; %bb.1:\n\ts_waitcnt vmcnt(0)\n")
     assert cp.violations(waited) == ([], 1)
+    # wait, THEN a new prefetch load, then the call in the same block: the earlier wait does not
+    # cover the later load -- flagged
+    late = ("_Zk:\n; %bb.1:\n\ts_waitcnt vmcnt(0)\n"
+            "\tglobal_load_dword v5, v[2:3], off ; mev-prefetch\n"
+            "\ts_swappc_b64 s[30:31], s[0:1]\n\ts_waitcnt vmcnt(63)\n\t; mev-prefetch-wait v5\n")
+    assert cp.violations(late)[0]
     text = open(cp.build_asm()).read()
     v, n = cp.violations(text)
     assert n >= 8 and v == []

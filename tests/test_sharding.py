@@ -109,8 +109,20 @@ def _bench_worker(rank, world, port, out_path):
     def collective():
         got["g"] = gather_final(reward, done)
 
-    elapsed, t_steps, t_coll = bench.timed_run(issue, plan, lambda: None, dist.barrier, collective)
+    calls = []
+
+    def slow_trailing_barrier():  # the region's second barrier call is the trailing one
+        calls.append(1)
+        if len(calls) == 2:
+            _t.sleep(0.3)
+        dist.barrier()
+
+    elapsed, t_steps, t_coll, t_bar = bench.timed_run(issue, plan, lambda: None,
+                                                      slow_trailing_barrier, collective)
     assert 0 < t_steps <= elapsed and 0 <= t_coll <= elapsed - t_steps + 1e-9
+    # the window ends at the gather's completion: the 0.3 s trailing barrier is not in it (the
+    # steps take 0.023 / 0.046 s per rank), and it is reported on its own
+    assert len(calls) == 2 and t_bar >= 0.3 and elapsed < 0.25
     mine = elapsed
     elapsed = bench.max_over_ranks(elapsed)
     every = [None] * world
@@ -173,6 +185,7 @@ def test_bench_spawns_its_own_ranks():
     wg = dd["warmup_gathers"]
     assert wg is not None and wg["final_ms"] > 0 and wg["obs_ms"] > 0
     assert 0 < dd["final_gather_ms"] <= out["ms_per_step"] * K
+    assert dd["trailing_barrier_ms"] >= 0 and "trailing barrier is outside" in dd["window"]
     assert 0 < dd["final_gather_share"] < 1
     assert dd["value_steps_only"] >= out["value"]
     rf = out["roofline"]

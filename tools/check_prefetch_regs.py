@@ -13,7 +13,8 @@ data landed) and no spill. This check, per kernel with prefetch loads:
     loaded registers (copies, spills, any use), other than further prefetch loads;
   * no instruction between them writes one (a register reused while the load is in flight);
   * no call (s_swappc / s_call) while one is in flight, unless an s_waitcnt vmcnt(0) precedes
-    it in its block: the callee's save / restore of a register it uses would lose the data.
+    it in its block, after the block's last prefetch load: the callee's save / restore of a
+    register it uses would lose the data.
 
 python tools/check_prefetch_regs.py [file.s]   (default: builds `make asm` and checks it)
 """
@@ -123,6 +124,7 @@ def check_kernel(name: str, lines):
             dst = regs_of(ops[0]) if ops else set()
             loaded |= dst
             inflight |= dst
+            vm_waited = False  # (only a vmcnt(0) wait after the last prefetch load counts)
             continue
         code = text.split(";")[0]
         if code.strip().endswith(":") or text.startswith("; %bb."):
