@@ -19,7 +19,8 @@ Contract (see DESIGN.md "Measurement"):
   launches (mev_step(1), the Gym ``step()``) instead.
 * Warmup: W steps, and then more until ``--warmup-floor-s`` seconds of back-to-back launches
   have run (untimed; the chip reaches its steady clock -- a 5-step warmup would time a cold
-  launch). ``warmup`` in the line is W as requested; ``warmup_executed`` what ran.
+  launch), then one untimed rehearsal of the timed region (its launches, gather and syncs).
+  ``warmup`` in the line is W as requested; ``warmup_executed`` what ran.
 * Timed region: barrier + synchronize, then the clock runs over the K steps and, when N > 1, a
   synchronize and the single final all-gather of the (reward, done) batch over RCCL, to the
   synchronize after it; the trailing barrier is outside the window (timed on its own,
@@ -343,6 +344,11 @@ def main():
                     help="HIP host wait policy for synchronize (hipSetDeviceFlags before the "
                          "device is initialised): auto (HIP's default), spin, blocking")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearsals", type=int, default=20,
+                    help="untimed runs of the timed region at the end of the warmup")
+    ap.add_argument("--timed-repeats", type=int, default=1,
+                    help="dev A/B: run the timed region this many more times after the measured "
+                         "one and report their windows (`timed_repeats_ms`); value stays the first")
     ap.add_argument("--profile-run", action="store_true",
                     help="minimal run for rocprofv3 (no CPU baseline, no step roofline)")
     ap.add_argument("--stub-engine", action="store_true",
@@ -496,10 +502,25 @@ def main():
         if n not in launchers:
             launchers[n] = eng.launcher(n, traj)
     barrier = dist.barrier if world > 1 else (lambda: None)
+    # the last warmup piece: untimed rehearsals of the timed region itself (the same launches,
+    # gather and synchronisation; --rehearsals, at most ~0.1 s of them), so that the measured
+    # region is not the first run of its host code path and of its isolated-launch rhythm -- the
+    # first run of a one-launch region measured ~7-9 us (4-5 %) slower than every later one in
+    # the same process (tools/gpu_bench_driver.sh)
+    t_r = time.perf_counter()
+    for _ in range(args.rehearsals):
+        timed_run(issue, plan, sync, barrier, collective if world > 1 else None)
+        warm += sum(plan)
+        if time.perf_counter() - t_r > 0.1:
+            break
     elapsed, t_steps, t_gather, t_barrier = timed_run(issue, plan, sync, barrier,
                                                       collective if world > 1 else None)
     elapsed = max_over_ranks(elapsed, device)
     t_barrier = max_over_ranks(t_barrier, device)
+    repeats = []
+    for _ in range(max(0, args.timed_repeats - 1)):
+        repeats.append(max_over_ranks(timed_run(issue, plan, sync, barrier,
+                                                collective if world > 1 else None)[0], device) * 1e3)
     t_steps = max_over_ranks(t_steps, device)
     t_gather = max_over_ranks(t_gather, device) if t_gather is not None else None
     if "rd" in gathered:
@@ -613,6 +634,7 @@ def main():
             "roofline": roof,
             "roofline_step": step_roof,
             "cpu_baseline": cpu,
+            **({"timed_repeats_ms": repeats} if repeats else {}),
             "distributed": ({"world_size_seen": dist.get_world_size(),
                              "backend": dist.get_backend(),
                              "final_gather_ms": t_gather * 1e3,
