@@ -262,8 +262,8 @@ def test_reward_guard_partial_band_same_rows_every_shape(size, k):
     got["packed_step"] = np.stack(rows)
     eng.close()
     ref = got["lds2_pipelined"]
-    for k, v in got.items():
-        np.testing.assert_array_equal(v, ref, err_msg=f"{k} vs lds2_pipelined")
+    for kind, v in got.items():
+        np.testing.assert_array_equal(v, ref, err_msg=f"{kind} vs lds2_pipelined")
     ob = OracleBatch(OracleParams(), L["bs"], U, seeds)
     want = np.stack([ob.step()["metrics"][:, 2] for _ in range(n)])
     np.testing.assert_allclose(ref, want, rtol=1e-5, atol=0)

@@ -170,7 +170,9 @@ def test_bench_spawns_its_own_ranks():
     assert out["n_gpus"] == 2 and out["steps"] == K and out["config"]["global_envs"] == 2 * E
     dd = out["distributed"]
     assert dd["world_size_seen"] == 2 and dd["backend"] == "gloo"
-    steps = W + K
+    # the warmup's W steps plus its untimed rehearsals of the timed region (whole plans of K)
+    assert out["warmup_executed"] >= W and (out["warmup_executed"] - W) % K == 0
+    steps = out["warmup_executed"] + K
     seeds = 1000 + np.arange(2 * E)
     assert dd["final_batch"]["shape"] == [2, 2, E]
     assert dd["final_batch"]["reward_sum"] == float((seeds + steps).sum())
