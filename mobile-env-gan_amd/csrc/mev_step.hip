@@ -1040,8 +1040,9 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
           ? valid_w
           : bal(t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0)) &
                 valid_w;
-  const bool need = active && wp.x < 0;
-  const uint64_t mneed_w = bal(wp.x < 0) & act_w;
+  const bool nowp = wp.x == -1;  // (no waypoint: see lds2_step)
+  const bool need = active && nowp;
+  const uint64_t mneed_w = bal(nowp) & act_w;
   int tot, rank;  // draws of this env this step (2 per waypoint); this lane's rank among them
   if constexpr (ROWS) {
     const uint32_t f = seg_field<PC>(mneed_w, m);
@@ -1325,15 +1326,28 @@ __device__ __forceinline__ bool packed_group(const KParams& kp, const KState& st
   if constexpr (LEAN) {
     // (the rare path's constants from the LDS blob's RewardC where there is one)
     const char* rcp = LDSA ? lblob + KPS(lds_r100_off) + 8 * kRewardCSlot : nullptr;
-    const bool risky = env_ok && leader && nact > 0 &&
-                       (ISUM ? (uint32_t)abs(isum_u) <= (uint32_t)nact * (uint32_t)kp.r_thr25
-                             : fabsf((float)sum_u) <= (float)nact * kp.r_thr);
-    if (bal(risky)) {
+    // (every UE active, aligned segments: the test as one unsigned compare, its ballot ANDed in
+    // SALU with the env leaders' lanes -- see lds2_step)
+    uint64_t risk_w;
+    if constexpr (ISUM && scn_all_active<SCN>()) {
+      constexpr uint64_t kLeadPat = [] {
+        uint64_t v = 0;
+        for (int q = 0; q < 64 / (PC ? PC : 64); ++q) v |= 1ull << (q * PC + PC - 1);
+        return v;
+      }();
+      const uint32_t T = (uint32_t)U * (uint32_t)kp.r_thr25;
+      risk_w = bal((uint32_t)isum_u + T <= 2u * T) & (envok_w & kLeadPat);
+    } else {
+      risk_w = bal(env_ok && leader && nact > 0 &&
+                   (ISUM ? (uint32_t)abs(isum_u) <= (uint32_t)nact * (uint32_t)kp.r_thr25
+                         : fabsf((float)sum_u) <= (float)nact * kp.r_thr));
+    }
+    if (risk_w) {
       wait_vmem();  // (no load in flight across the call)
       const RewardC c = LDSA ? reward_c(rcp)
                              : RewardC{tb.util, kp.util_sat, (double)kp.util_kmax, kp.u_err, 0};
       const float ex = packed_fix<ROWS, PC>(active ? cents : -1.0, U, u, c.tab, c.kmax, c.sat, nact);
-      use_exact = risky;
+      use_exact = (risk_w >> __lane_id()) & 1ull;
       exact_r = ex;
     }
   }
@@ -1745,7 +1759,8 @@ struct Ctx2 {
 // LDS cell map of the closest station within any pair's reach, s*, which serves the UE when the
 // (class of s*, UE class) pair connects at that distance -- the closest station overall is then
 // the closest connectable one, ties by index included -- else from the UE class's L2 map.
-template <int UC, int SCN, int R, bool PE, bool TF = false, bool FULL = false, bool HET = false>
+template <int UC, int SCN, int R, bool PE, bool TF = false, bool FULL = false, bool HET = false,
+          bool RT1 = false>
 __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, const KOut& out,
                                           const KTables& tb, const LaneMap& m, Ctx2 (&c)[R],
                                           const int (&e)[R], const int (&nok)[R], int kval,
@@ -1808,8 +1823,11 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
                     (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
     active[r] = valid[r] && on;
     act_w[r] = scn_all_active<SCN>() ? valid_w[r] : bal(on) & valid_w[r];
-    need[r] = active[r] && c[r].wp.x < 0;
-    mneed_w[r] = bal(c[r].wp.x < 0) & act_w[r];
+    // (no waypoint: wp.x == -1 exactly; as `< 0` the compiler formed the predicate twice, as a
+    // shift and as a mask test, each with its own compare)
+    const bool nowp = c[r].wp.x == -1;
+    need[r] = active[r] && nowp;
+    mneed_w[r] = bal(nowp) & act_w[r];
     const uint32_t f = seg_field<PC>(mneed_w[r], m);
     tot[r] = __popc(f);
     rank[r] = __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)u));
@@ -2093,26 +2111,59 @@ __device__ __forceinline__ void lds2_step(const KParams& kp, const KState& st, c
     // (reward_risky, rare: the exact reward's float32 bits instead, flag 0x100; the constants
     // from the blob's RewardC)
     const char* rcp = lblob + KPS(lds_r100_off) + 8 * kRewardCSlot;
-    const bool risky = lead && nact > 0 && (uint32_t)abs(isum) <= (uint32_t)nact * (uint32_t)kp.r_thr25;
-    int word0 = isum, flag = 0;
-    if (bal(risky)) {
-      // (every load landed before the call: the next pair's prefetch registers are not tracked
-      // by the compiler, and a callee's save / restore of one in flight would lose its data;
-      // tools/check_prefetch_regs.py checks the wait)
-      wait_vmem();
-      const RewardC rc = reward_c(rcp);
-      const float ex = packed_fix<true, PC>(active[r] ? (double)cf[r] : -1.0, U, u, rc.tab, rc.kmax,
-                                            rc.sat, nact);
-      if (risky) {
-        word0 = __float_as_int(ex);
-        flag = 0x100;
-      }
-    }
     const int er = r * G + m.seg;
     int* const hw = h[r] + min(u, PC - 2);
     int* sw = lead ? srow + 2 * er : hw;
-    sw[0] = word0;
-    sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0) | flag;
+    if constexpr (RT1 && scn_all_active<SCN>()) {
+      // RT1 (short launches of the scenario instances): |isum| <= T = nact r_thr25 (every UE
+      // active: nact = U > 0) as one unsigned compare, (uint)(isum + T) <= 2T (|isum| <= U 2^25
+      // and T <= U 2^25: no wrap across the band), its ballot ANDed in SALU with the lanes that
+      // store the env rows (u = PC - 1 of the envs that exist: the ballot of `lead` itself costs
+      // two VALU), and the risky flag set in the rare branch only. Measured (interleaved, four
+      // boxes): 20-step launches at 65,536 large envs 161.5-162.3 vs 165.1-166.3 us, 200-step
+      // launches 1.52-1.53 vs 1.48-1.50 ms on three of the boxes (long launches are store-bound,
+      // and the cheaper step did not make them faster) -- the host takes it for launches of
+      // fewer than 64 steps only
+      constexpr uint64_t kLeadPat = [] {
+        uint64_t v = 0;
+        for (int q = 0; q < 64 / PC; ++q) v |= 1ull << (q * PC + PC - 1);
+        return v;
+      }();
+      int word0 = isum;
+      int word1 = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0);
+      const uint32_t T = (uint32_t)U * (uint32_t)kp.r_thr25;
+      const uint64_t risk_w = bal((uint32_t)isum + T <= 2u * T) & (envok_w[r] & kLeadPat);
+      if (risk_w) {
+        wait_vmem();  // (no prefetch in flight across the call: see below)
+        const RewardC rc = reward_c(rcp);
+        const float ex = packed_fix<true, PC>(active[r] ? (double)cf[r] : -1.0, U, u, rc.tab,
+                                              rc.kmax, rc.sat, nact);
+        if ((risk_w >> __lane_id()) & 1ull) {
+          word0 = __float_as_int(ex);
+          word1 |= 0x100;
+        }
+      }
+      sw[0] = word0;
+      sw[1] = word1;
+    } else {
+      const bool risky = lead && nact > 0 && (uint32_t)abs(isum) <= (uint32_t)nact * (uint32_t)kp.r_thr25;
+      int word0 = isum, flag = 0;
+      if (bal(risky)) {
+        // (every load landed before the call: the next pair's prefetch registers are not
+        // tracked by the compiler, and a callee's save / restore of one in flight would lose its
+        // data; tools/check_prefetch_regs.py checks the wait)
+        wait_vmem();
+        const RewardC rc = reward_c(rcp);
+        const float ex = packed_fix<true, PC>(active[r] ? (double)cf[r] : -1.0, U, u, rc.tab,
+                                              rc.kmax, rc.sat, nact);
+        if (risky) {
+          word0 = __float_as_int(ex);
+          flag = 0x100;
+        }
+      }
+      sw[0] = word0;
+      sw[1] = nact | ((c[r].t + 1 >= KPS(t_end)) ? 0x80 : 0) | flag;
+    }
     c[r].t += 1;
   }
 }
@@ -2147,7 +2198,7 @@ __device__ __forceinline__ int pipe_pre(const KParams& kp, const LaneMap& m, con
   const bool on = scn_all_active<SCN>() ||
                   (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
   const uint64_t act_w = scn_all_active<SCN>() ? valid_w : bal(on) & valid_w;
-  const uint32_t f = seg_field<PC>(bal(c.wp.x < 0) & act_w, m);
+  const uint32_t f = seg_field<PC>(bal(c.wp.x == -1) & act_w, m);  // (no waypoint: see lds2_step)
   const int k = c.drawn + __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)m.u));
   return ltab[m.seg * M + min(k, M - 1)];
 }
@@ -2202,8 +2253,9 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
                   (t >= KPS(arr_start) && t < KPS(arr_exit) && (KPS(first_step_active) || t != 0));
   const bool active = valid && on;
   const uint64_t act_w = scn_all_active<SCN>() ? valid_w : bal(on) & valid_w;
-  const bool need = active && c.wp.x < 0;
-  const uint64_t mneed_w = bal(c.wp.x < 0) & act_w;
+  const bool nowp = c.wp.x == -1;  // (no waypoint: see lds2_step)
+  const bool need = active && nowp;
+  const uint64_t mneed_w = bal(nowp) & act_w;
   const uint32_t f = seg_field<PC>(mneed_w, m);
   const int tot = __popc(f);
   const int rank = __popc(__builtin_amdgcn_ubfe(f, 0u, (uint32_t)u));
@@ -2680,7 +2732,7 @@ __host__ __device__ inline size_t lds2_per_wave(int G, int B, int M, int R, bool
 // without cells beyond the mode-3 table's ranks)
 // HET: heterogeneous entities, shared layout (lds2_step's HET; the generic instance only)
 template <int UC, int SCN, bool PE = false, bool TF = false, int R = 2, bool C8 = scn_st8(SCN),
-          bool PIPE = false, bool HET = false>
+          bool PIPE = false, bool HET = false, bool RT1 = false>
 __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
     KParams kp, KState st, KOut out, KTables tb, int ngroups, int nsteps, int traj,
     int stage_rows) {
@@ -2787,7 +2839,7 @@ __global__ __launch_bounds__(64 * kLds2Waves) void k_steps_lds2(
         int i = 0, sr = 0;
         do {  // (nsteps >= 1: the loop body runs at least once)
           int* const win = sw + (dbl ? 2 * hcur * wrows : 0);
-          lds2_step<UC, SCN, R, PE, TF, decltype(full)::value, HET>(
+          lds2_step<UC, SCN, R, PE, TF, decltype(full)::value, HET, RT1>(
               kp, st, out, tb, m, c, e, nok, kval, klead, traj ? i : 0, lblob, lpcg, hist, ltab,
               win + 2 * (sr * NWG + wvu * G * R), lkeys, hpk, hvf, hml);
           if (!alt && (sr + 1 == stage_rows || i + 1 == nsteps)) {
@@ -5400,6 +5452,9 @@ static int launch_packed_steps(const mev_ctx* c, const KState& ks, const KOut& k
                               : k_steps_lds2<15, 1, false, false, 1, scn_st8(1), true>)
                         : (tf ? k_steps_lds2<30, 2, false, true, 1, scn_st8(2), true>
                               : k_steps_lds2<30, 2, false, false, 1, scn_st8(2), true>);
+      else if (R == 2 && tf && nsteps < 64 && (scn == 1 || scn == 2))  // (RT1: see lds2_step)
+        k2 = scn == 1 ? k_steps_lds2<15, 1, false, true, 2, scn_st8(1), false, false, true>
+                      : k_steps_lds2<30, 2, false, true, 2, scn_st8(2), false, false, true>;
       else if (R == 2)
         k2 = kp.U == 15 ? (scn == 1 ? (tf ? k_steps_lds2<15, 1, false, true> : k_steps_lds2<15, 1>)
                            : c8     ? k_steps_lds2<15, 0, false, false, 2, true>

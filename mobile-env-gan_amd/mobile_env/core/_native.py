@@ -169,8 +169,11 @@ def lib():
         L.mev_strerror.argtypes = [C.c_int]
         L.mev_strerror.restype = C.c_char_p
         L.mev_last_hip_error.restype = C.c_char_p
-        if L.mev_abi_version() != ABI_VERSION:
-            raise ImportError(f"libmev ABI {L.mev_abi_version()} != expected {ABI_VERSION}")
+        # (MEV_LIB, dev A/B of library variants: a variant of the previous ABI is accepted -- the
+        # ABI changes between neighbouring versions are additive)
+        abi = L.mev_abi_version()
+        if abi != ABI_VERSION and not (os.environ.get("MEV_LIB") and abi == ABI_VERSION - 1):
+            raise ImportError(f"libmev ABI {abi} != expected {ABI_VERSION}")
         L.mev_source_hash.restype = C.c_char_p
         built, src = L.mev_source_hash().decode(), source_hash()
         if src is not None and built != src and not os.environ.get("MEV_LIB"):

@@ -272,3 +272,36 @@ def test_reward_guard_partial_band_same_rows_every_shape(size, k):
     inside, outside = np.abs(want) < 0.9 * thr, np.abs(want) > 1.1 * thr
     assert inside.mean() > 0.005 and outside.mean() > 0.005, (thr, inside.mean(), outside.mean())
     np.testing.assert_allclose(ref[inside], want[inside].astype(np.float32), rtol=1.2e-7, atol=0)
+
+
+def test_small_deferred_reward_guard_same_rows_as_step():
+    """mobile-small's LDS-table rollout marks reward-risky env-steps in an LDS bit map and
+    re-forms them after the group's steps (k_steps_packed DEFR, ~1 % of small's env-steps are
+    risky at the default band) instead of in the step: its rewards equal the one-step launches'
+    (in-step exact path) bit for bit, over 45 steps (two resets) and with the band 3x wider, and
+    are within 1e-5 relative (atol 0) of the oracle's float64 means."""
+    from mobile_env.core.engine import EngineParams, StepEngine
+    from mobile_env.scenarios.registry import LAYOUTS
+    from oracle.vec import OracleBatch, OracleParams
+    L = LAYOUTS["small"]
+    U, B, E, n = L["num_ues"], len(L["bs"]), 3000, 45
+    seeds = 90001 + 5 * np.arange(E)
+    ob = OracleBatch(OracleParams(), L["bs"], U, seeds)
+    want = np.stack([ob.step()["metrics"][:, 2] for _ in range(n)])
+    for rex in (0, -3):
+        eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B, reward_exact=rex),
+                         L["bs"], seeds, device="cuda")
+        tr = eng.rollout(n)
+        assert eng.last_launch_kind == "packed_fused"
+        fused = tr.reward.cpu().numpy()
+        eng.close()
+        eng = StepEngine(EngineParams(num_envs=E, num_ues=U, num_bs=B, reward_exact=rex),
+                         L["bs"], seeds, device="cuda")
+        rows = []
+        for _ in range(n):
+            eng.step()
+            rows.append(eng.reward.cpu().numpy())
+        assert eng.last_launch_kind == "packed_step"
+        eng.close()
+        np.testing.assert_array_equal(fused, np.stack(rows), err_msg=f"reward_exact {rex}")
+        np.testing.assert_allclose(fused, want, rtol=1e-5, atol=0, err_msg=f"reward_exact {rex}")

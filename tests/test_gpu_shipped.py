@@ -83,6 +83,33 @@ def test_large_65536_bench_rollout_strided_vs_oracle():
     torch.cuda.empty_cache()
 
 
+def test_large_bench_short_and_long_launch_instances_agree():
+    """The two-group scenario kernel comes in two instances by launch length (lds2_step RT1: the
+    one-compare reward test for launches of fewer than 64 steps -- the driver's 20-step shape --
+    and the original test for longer ones): a 70-step launch and a 20-step launch of the same
+    65,536 envs give the same first 20 rows bit for bit, and the long launch's 70 rows match the
+    oracle on every 16th env."""
+    import mobile_env
+    import torch
+    E, stride = 65536, 16
+    rows = {}
+    for n in (20, 70):
+        env = mobile_env.make("mobile-large-central-v0", num_envs=E, device="cuda:0", seed=4242)
+        env.reset()
+        eng = env.engine
+        tr = eng.rollout(n)
+        assert eng.last_launch_kind == "lds2_two_groups"
+        rows[n] = [x[:20].cpu().numpy() for x in (tr.obs, tr.serving, tr.reward, tr.done)]
+        if n == 70:
+            idx = np.arange(0, E, stride)
+            assert_rollout_vs_oracle(tr, _oracle("large", env.seeds.numpy()[idx]), n, env_idx=idx)
+        del tr
+        env.close()
+        torch.cuda.empty_cache()
+    for a, b, name in zip(rows[20], rows[70], ("obs", "serving", "reward", "done")):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+
+
 @pytest.mark.parametrize("env_id,size,E,stride", [("mobile-medium-central-v0", "medium", 4096, 1),
                                                   ("mobile-large-central-v0", "large", 65536, 16)])
 def test_gym_step_shipped_vs_oracle(env_id, size, E, stride):
