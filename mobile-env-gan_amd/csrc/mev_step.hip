@@ -344,6 +344,33 @@ __device__ __forceinline__ int2 step_v15(int2 pos, int dx, int dy, int ax2, int 
   const int sy = (ay2 << 3 > ax2 ? 1 : 0) + (dx == 0 && !(pos.y & 1) ? 1 : 0);
   return make_int2(pos.x + (dx < 0 ? -sx : sx), pos.y + (dy < 0 ? -sy : sy));
 }
+// step_v15 in fewer VALU: [8 dx^2 > dy^2] as the sign bit of dy^2 - 8 dx^2 (one 24-bit
+// multiply-add and a shift), and x + sgn(dx) sx as one 24-bit multiply-add with sgn(dx) =
+// med3(dx, -1, 1): 24 instead of 29 VALU per UE and step with the selects. (The two as inline
+// assembly: written in C, the compiler turned the multiply by -8 into a shift pair and the clamp
+// of wp.x - x into two compares and two selects against the coordinates.) dx = 0 gives sgn 0
+// and, off the arrival radius, sx = 0 as well, so the product is the step either way. Taken by
+// the software-pipelined loop (4,096 medium envs, one wave per SIMD: 90.4 vs 95.6 us per
+// 200-step launch, interleaved); in the two-group loop it measured slower (20-step 163.8 vs
+// 162.6 us, 200-step 1.54 vs 1.49 ms -- as for every step shortened there) and the
+// Gym step() unchanged, so those keep step_v15.
+__device__ __forceinline__ int mad_m8_i24(int a, int c) {  // c - 8 a (|a| < 2^23)
+  int r;
+  asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(r) : "v"(a), "v"(c));
+  return r;
+}
+__device__ __forceinline__ int sgn_i32(int x) {  // med3(x, -1, 1)
+  int r;
+  asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ int2 step_v15_mad(int2 pos, int dx, int dy, int ax2, int ay2) {
+  const int gx = (int)((uint32_t)mad_m8_i24(ax2, ay2) >> 31);  // 8 dx^2 > dy^2
+  const int gy = (int)((uint32_t)mad_m8_i24(ay2, ax2) >> 31);  // 8 dy^2 > dx^2
+  const int sx = gx + (((pos.x & 1) | dy) == 0 ? 1 : 0);  // (dy == 0 and x even: |step| 2)
+  const int sy = gy + (((pos.y & 1) | dx) == 0 ? 1 : 0);
+  return make_int2(__mul24(sgn_i32(dx), sx) + pos.x, __mul24(sgn_i32(dy), sy) + pos.y);
+}
 // Movement step. Arrival (|v| <= velocity) is the integer test d2 <= d2snap (sqrt is
 // correctly rounded and monotone). Otherwise the new coordinate is x + rint(q) with
 // q = velocity * dx / |v| (x is an integer, so rint(x + q) = x + rint(q) unless x + q is a
@@ -2302,7 +2329,7 @@ __device__ __forceinline__ Snap pipe_move(const KParams& kp, const KTables& tb, 
   const bool arrive = d2 <= KPS(d2snap);
   int2 npos;
   if (V15 || KPS(axis_exact) == 2) {
-    int2 np = step_v15(pos, dx, dy, ax2, ay2);
+    int2 np = step_v15_mad(pos, dx, dy, ax2, ay2);
     asm volatile("" : "+v"(np.x), "+v"(np.y));  // (a select, not a branch on `arrive`)
     npos = arrive ? wp : np;
   } else {
