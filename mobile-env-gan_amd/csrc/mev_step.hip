@@ -4961,17 +4961,21 @@ static int create_ctx(mev_ctx* c, const mev_params* params) {
     if (std::isfinite(kmax) && kmax < (double)(1 << 22)) {
       kp.util_direct = 0;
       kp.util_kmax = (int)kmax;
-      // the float32 utility's absolute error (utility_f32r), twice the sum of: the rate's float32
+      // the float32 utility's absolute error (utility_f32r), the sum of: the rate's float32
       // rounding and w2's (3 ulp relative, 2.2e-8 for 0.01f) through log2 (1 / ln 2 per relative
-      // unit) times the slope A = |w1 ln2 / ln w3 * scale|; v_log_f32 (taken as 2 ulp of
-      // max(|log2 x|, 1) over the table's rates, x = w2 + 0.01 .. w2 + r_sat); the products,
-      // clip bounds and offset (2 ulp each of max(|lower|, |upper|) * scale, 1, |offset|)
+      // unit) times the slope A = |w1 ln2 / ln w3 * scale|; v_log_f32 (taken as 2^-22
+      // max(|log2 x|, 1) over the table's rates, x = w2 + 0.01 .. w2 + r_sat: twice its measured
+      // worst case, 0.993 * 2^-23 max(|log2 x|, 1) over every float32 x in [2^-8, 2^8),
+      // tools/log2_probe.hip); the products, clip bounds and offset (2 ulp each of
+      // max(|lower|, |upper|) * scale, 1, |offset|, where their roundings come to <= 1 ulp).
+      // (Rounds <= 5 doubled this sum: at the defaults a band of |mean| <= 0.166 instead of
+      // 0.086, which took 8.3 % of mobile-small's env-steps to the exact path instead of 2.7 %.)
       const double A = fabs(kp.w1 * log(2.0) / kp.log_w3 * (2.0 / (kp.upper - kp.lower)));
       const double lmax = std::max({1.0, fabs(log2(kp.w2 + 0.01)), fabs(log2(kp.w2 + std::max(r_sat, 0.01)))});
       const double off = fabs(-2.0 * kp.lower / (kp.upper - kp.lower) - 1.0);
       const double sc = std::max(fabs(kp.lower), fabs(kp.upper)) * 2.0 / (kp.upper - kp.lower);
-      kp.u_err = (float)(2.0 * (A * ((3.0 * 0x1p-24 + 2.2e-8) / log(2.0) + 0x1p-22 * lmax) +
-                               0x1p-22 * (1.0 + off + sc)));
+      kp.u_err = (float)(A * ((3.0 * 0x1p-24 + 2.2e-8) / log(2.0) + 0x1p-22 * lmax) +
+                         0x1p-22 * (1.0 + off + sc));
       if (params->reward_exact > 0) kp.u_err = INFINITY;  // (every row takes the exact path)
       // (tests: a band -reward_exact times wider, so that a subset of rows takes the exact path)
       if (params->reward_exact < -1) kp.u_err *= (float)-params->reward_exact;

@@ -193,18 +193,18 @@ def _u_err(lower, upper, w1, w2, w3):
     lmax = max(1.0, abs(math.log2(w2 + 0.01)), abs(math.log2(w2 + max(r_sat, 0.01))))
     off = abs(-2.0 * lower / (upper - lower) - 1.0)
     sc = max(abs(lower), abs(upper)) * 2.0 / (upper - lower)
-    return 2.0 * (A * ((3.0 * 2.0 ** -24 + 2.2e-8) / math.log(2.0) + 2.0 ** -22 * lmax)
-                  + 2.0 ** -22 * (1.0 + off + sc))
+    return (A * ((3.0 * 2.0 ** -24 + 2.2e-8) / math.log(2.0) + 2.0 ** -22 * lmax)
+            + 2.0 ** -22 * (1.0 + off + sc))
 
 
 @pytest.mark.parametrize("lower,upper,coeffs", [(-20.0, 20.0, (10.0, 0.0, 10.0)),
                                                 (-5.0, 8.0, (4.0, 0.5, 2.0))])
 def test_float32_utility_within_the_guards_bound(lower, upper, coeffs):
     """The reward guard (reward_risky) rests on a bound u_err on the float32 utility's error
-    (utility_f32r: the hardware log2 taken as 2 ulp, every rounding counted, then doubled). On
-    every active UE of a lean 45-step rollout (the shipped scenario instance at the defaults, the
-    generic one at other utility parameters) the obs utility is within HALF that bound of the
-    oracle's float64 utility -- the factor-2 margin holds on the hardware."""
+    (utility_f32r: the hardware log2 taken as twice its measured worst case, tools/log2_probe.hip,
+    every rounding counted at 2 ulp). On every active UE of a lean 45-step rollout (the shipped
+    scenario instance at the defaults, the generic one at other utility parameters) the obs
+    utility is within that bound of the oracle's float64 utility."""
     from mobile_env.core.engine import EngineParams, StepEngine
     from mobile_env.scenarios.registry import LAYOUTS
     from oracle.vec import OracleBatch, OracleParams
@@ -225,15 +225,15 @@ def test_float32_utility_within_the_guards_bound(lower, upper, coeffs):
         worst = max(worst, float(np.max(np.abs(u[act] - o["util"][act]))))
     eng.close()
     bound = _u_err(lower, upper, *coeffs)
-    assert worst <= bound / 2, (worst, bound)
+    assert worst <= bound, (worst, bound)
 
 
-@pytest.mark.parametrize("size,k", [("large", 5), ("medium", 3)])
+@pytest.mark.parametrize("size,k", [("large", 10), ("medium", 6)])
 def test_reward_guard_partial_band_same_rows_every_shape(size, k):
     """The reward guard decides which env-steps take the exact path with ONE test in every
     kernel shape (the 2^-25 fixed-point sum against nact r_thr25): the two-group step's in-step
     test, the pipelined loop's flush (DETECT), the packed kernels' leaders. With the band made k
-    times wider (reward_exact = -k: |mean| up to ~0.81 / ~0.49 instead of 0.166, which no
+    times wider (reward_exact = -k: |mean| up to ~0.81 / ~0.49 instead of 0.086, which no
     large / medium env-step reaches) a subset of the rows -- some, not all -- takes the exact
     path; every shape then gives the same reward bits, the rows well inside the band are within
     one float32 ulp of the oracle's float64 mean (the exact path), and every row within 1e-5
@@ -275,11 +275,11 @@ def test_reward_guard_partial_band_same_rows_every_shape(size, k):
 
 
 def test_small_deferred_reward_guard_same_rows_as_step():
-    """mobile-small's LDS-table rollout marks reward-risky env-steps in an LDS bit map and
-    re-forms them after the group's steps (k_steps_packed DEFR, ~1 % of small's env-steps are
-    risky at the default band) instead of in the step: its rewards equal the one-step launches'
-    (in-step exact path) bit for bit, over 45 steps (two resets) and with the band 3x wider, and
-    are within 1e-5 relative (atol 0) of the oracle's float64 means."""
+    """mobile-small is the registered workload whose env-steps reach the reward guard's band
+    (2.7 % of them at the default band, |mean| <= 0.086): its LDS-table rollout's rewards
+    (k_steps_packed, in-step exact path) equal the one-step launches' bit for bit, over 45 steps
+    (two resets) and with the band 3x wider, and are within 1e-5 relative (atol 0) of the
+    oracle's float64 means."""
     from mobile_env.core.engine import EngineParams, StepEngine
     from mobile_env.scenarios.registry import LAYOUTS
     from oracle.vec import OracleBatch, OracleParams
